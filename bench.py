@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mode S (Census -> Hamming -> 8-path SGM -> WTA) in
+Mdisparities/s (W*H*D per second) at 1920x1080, D=128 (BASELINE.json config 2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one full disparity computation of one synthetic 1080p pair per rank
+(inputs already resident in HBM), followed for N > 1 by the path's one
+exchange: an RCCL gather of the u16 disparity maps to rank 0 over xGMI.
+Pairs are independent units (weak scaling: every rank matches its own pair).
+Rank 0 prints one JSON line (the driver's contract), including the live
+hipEvent roofline of the dominant kernel and the CPU baseline (the oracle,
+single thread, the same 1080p D=128 frame) timed on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+AGG_BYTES_PER_DISP = 10.0      # 8 u8 C reads + 1 u16 S write
+
+WORKLOADS = {
+    "1080p_d128": dict(W=1920, H=1080, D=128),   # BASELINE configs[1]
+    "4k_d256": dict(W=3840, H=2160, D=256),      # BASELINE configs[2]
+    "1080p_d192": dict(W=1920, H=1080, D=192),   # BASELINE configs[4] per-pair shape
+    "vga_d64": dict(W=640, H=480, D=64),         # BASELINE configs[0] shape
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="1080p_d128", choices=sorted(WORKLOADS))
+    ap.add_argument("--pairs-per-rank", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=1)
+    return ap.parse_args()
+
+
+def cpu_baseline(W, H, D, threads):
+    """Oracle ('port') timing on this host: the same frame the GPU computes."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle  # CPU baseline leg only
+    from stereovisionarray_amd import synth
+    L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=1)
+    t0 = time.perf_counter()
+    pyoracle.sgm(L, R, D, 0, -1, 10, 120, subpixel=True, threads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(W * H * D / dt / 1e6, 3),
+        "unit": "Mdisp/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"oracle/sgm_oracle.c svo_sgm, one full {W}x{H} D={D} frame "
+                  f"(census+cost+8 paths+WTA+subpixel), {threads} thread(s), {dt:.2f} s",
+    }
+
+
+def load_traffic(workload):
+    """HBM bytes per sgm_paths launch from the committed rocprofv3 PMC pass
+    (profiles/pmc_<workload>.json, written by tools/pmc_traffic.py), or None."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("kernels", {}).get("sgm_paths", {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    import stereovisionarray_amd as sva
+    from stereovisionarray_amd import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    wl = WORKLOADS[a.workload]
+    W, H, D = wl["W"], wl["H"], wl["D"]
+    P = a.pairs_per_rank
+    params = sva.default_params(D=D, dmin=0, dir=-1, subpixel=1)
+    ctx = sva.Context(local)
+    stream = torch.cuda.Stream(dev)     # non-default stream shared by kernels, copies, RCCL
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
+    ctx.reserve(W, H, D)
+
+    lefts, rights = [], []
+    for j in range(P):
+        L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=1 + rank * P + j)
+        lefts.append(torch.from_numpy(L).to(dev))
+        rights.append(torch.from_numpy(R).to(dev))
+    disp = torch.zeros((P, H, W), dtype=torch.int16, device=dev)
+    sub = torch.zeros((P, H, W), dtype=torch.float32, device=dev)
+    gathered = (torch.zeros((world, P, H, W), dtype=torch.int16, device=dev)
+                if world > 1 and rank == 0 else None)
+
+    def step():
+        for j in range(P):
+            ctx.disparity_sgm_d(lefts[j].data_ptr(), rights[j].data_ptr(), W, H, W, params,
+                                disp[j].data_ptr(), sub[j].data_ptr())
+        if world > 1:   # the path's one exchange: disparity maps -> rank 0
+            dist.gather(disp, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kernels = {}
+    for name in ("census", "cost", "sgm_paths", "wta"):
+        ms, n = ctx.kernel_time(name)
+        if n:
+            kernels[name] = {"avg_ms": ms / n, "launches": n}
+    # sanity: the result is a real disparity map (exact on the stripe interiors)
+    d0 = disp[0].cpu().numpy().view(np.uint16)
+    assert d0.max() < D, "disparity out of range"
+
+    units = world * P * a.steps
+    disparities = units * W * H * D
+    value = disparities / elapsed / 1e6
+    ms_per_step = elapsed / a.steps * 1e3
+    agg = kernels.get("sgm_paths")
+    roofline = None
+    if agg:
+        alg_bytes = AGG_BYTES_PER_DISP * W * H * D
+        achieved = alg_bytes / (agg["avg_ms"] * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": load_traffic(a.workload),
+                    "kernel": "sgm_paths", "kernel_avg_ms": round(agg["avg_ms"], 4),
+                    "alg_bytes_per_launch": alg_bytes}
+    out = {
+        "metric": "Mdisparities/sec (W·H·D/s) at 1080p D=128" if a.workload == "1080p_d128"
+                  else f"Mdisparities/sec (W·H·D/s) {a.workload}",
+        "value": round(value, 1),
+        "unit": "Mdisp/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic (MT19937 u8 texture, 16-stripe piecewise-constant disparity)",
+        "config": {"workload": f"{W}x{H} D={D} Mode S SGM (census 9x7, Hamming, 8 paths, "
+                               f"WTA+subpixel), {P} pair(s)/rank",
+                   "W": W, "H": H, "D": D, "P1": 10, "P2": 120,
+                   "parallelism": f"pairs sharded over {world} rank(s), RCCL gather to rank 0"},
+        "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
+        "roofline": roofline,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(W, H, D, a.cpu_threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,160 @@
+/*
+ * sva.h -- C-ABI of libsva.so, the MI355X-native stereo disparity engine.
+ *
+ * This is the drop-in boundary for the reference's array-stereo cost-volume
+ * path.  The reference (Nahuel-M/StereoVisionArray) has no plugin API: its hot
+ * loop is written inline in main() (src/CameraStereoVision.cpp:44-95) and
+ * reaches helpers through include/functions.h and include/Camera.h.  Each
+ * entry point below names the reference code it replaces.
+ *
+ * Conventions
+ *   - extern "C", plain pointers and sizes, no C++/torch types.
+ *   - Every function returns an int status: SVA_OK (0) or an SVA_ERR_* code.
+ *     No exception crosses the ABI.  sva_last_error() gives the message of the
+ *     last failing call on that context.
+ *   - Functions without suffix take HOST buffers and are synchronous.
+ *     Functions with suffix _d take DEVICE buffers (hipMalloc'd on the
+ *     context's device) and are asynchronous on the context's stream; call
+ *     sva_synchronize() (or synchronise the stream yourself) before reading.
+ *   - Images are 8-bit grayscale, row-major, row pitch in bytes (>= width).
+ *     Every other array is dense (pitch = width).
+ *   - A context owns one device and one stream and is not re-entrant; calls on
+ *     different contexts may run concurrently from different host threads.
+ *   - There is no CPU fallback: if no HIP device is usable every compute call
+ *     fails with SVA_ERR_NO_DEVICE.
+ */
+#ifndef SVA_H
+#define SVA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SVA_ABI_VERSION 1
+
+enum {
+    SVA_OK = 0,
+    SVA_ERR_INVALID_ARG = 1,   /* bad size / pointer / parameter            */
+    SVA_ERR_UNSUPPORTED = 2,   /* parameter combination not built           */
+    SVA_ERR_DEVICE = 3,        /* HIP runtime error                         */
+    SVA_ERR_OUT_OF_MEMORY = 4, /* workspace allocation failed               */
+    SVA_ERR_NO_DEVICE = 5      /* no usable HIP device                      */
+};
+
+/* Mirrors class Camera (include/Camera.h:6-21): public f, pos3D, pixel_size. */
+typedef struct sva_camera {
+    double f;
+    double pos[3];
+    double pixel_size;
+} sva_camera;
+
+/* Mode S parameters.  Use sva_sgm_params_default(). */
+typedef struct sva_sgm_params {
+    int32_t D;           /* disparity count; GPU path: multiple of 32, 32..256     */
+    int32_t dmin;        /* first disparity                                        */
+    int32_t dir;         /* +1: match at x+(dmin+d) in the other image, -1: x-(..) */
+    int32_t P1;          /* small-jump penalty (default 10)                        */
+    int32_t P2;          /* large-jump penalty (default 120); 0 <= P1, P2 <= 193    */
+    int32_t subpixel;    /* 1: also write the f32 parabola sub-pixel map          */
+    int32_t lr_check;    /* 1: left/right consistency check       */
+    int32_t lr_max_diff; /* max |dL - dR| kept by the check (default 1)            */
+    uint16_t invalid;    /* disparity written for pixels the check rejects         */
+    uint16_t _pad;
+} sva_sgm_params;
+
+/* One stereo pair for the batch API. */
+typedef struct sva_pair_job {
+    const uint8_t* left;  /* host, reference image                  */
+    const uint8_t* right; /* host, matched image                    */
+    int32_t width, height;
+    size_t pitch;
+    uint16_t* disp;       /* host, width*height                     */
+    float* subpix;        /* host, width*height or NULL             */
+} sva_pair_job;
+
+/* ------------------------------------------------------------ context --- */
+void sva_sgm_params_default(sva_sgm_params* p);
+int sva_abi_version(void);
+int sva_device_count(int* count);
+int sva_create(int device, void** ctx_out);          /* sva_ctx* as void*   */
+int sva_destroy(void* ctx);
+/* Adopt an external hipStream_t (NULL = the context's own stream). */
+int sva_set_stream(void* ctx, void* hip_stream);
+int sva_synchronize(void* ctx);
+const char* sva_last_error(void* ctx);
+const char* sva_status_string(int status);
+/* Pre-size the workspace for W x H x D (optional; calls grow it on demand). */
+int sva_reserve(void* ctx, int width, int height, int D);
+
+/* Kernel timing with hipEvents on the context stream (measurement only). */
+int sva_set_timing(void* ctx, int enable);
+int sva_reset_timing(void* ctx);
+/* Total milliseconds and launch count of kernel `name` since the last reset. */
+int sva_kernel_time(void* ctx, const char* name, double* total_ms, int64_t* count);
+
+/* ------------------------------------------------------ Mode S (SGM) --- */
+/* Whole path: census -> Hamming cost -> 8-path SGM -> WTA (+ sub-pixel).
+ * Replaces the inline hot loop CameraStereoVision.cpp:44-95 with the
+ * north_star SGM matcher.  disp: W*H u16 (dmin + d*); subpix: W*H f32 or NULL. */
+int sva_disparity_sgm(void* ctx, const uint8_t* left, const uint8_t* right, int width,
+                      int height, size_t pitch, const sva_sgm_params* p, uint16_t* disp,
+                      float* subpix);
+int sva_disparity_sgm_d(void* ctx, const uint8_t* left, const uint8_t* right, int width,
+                        int height, size_t pitch, const sva_sgm_params* p, uint16_t* disp,
+                        float* subpix);
+
+/* Stage entry points (device buffers).  Layouts: census W*H u64; C, L
+ * [y][x][d] u8; S [y][x][d] u16; L volumes [8][y][x][d] (direction table in
+ * DESIGN.md §2.3). */
+int sva_census_d(void* ctx, const uint8_t* img, int width, int height, size_t pitch,
+                 uint64_t* census);
+int sva_cost_d(void* ctx, const uint64_t* census_l, const uint64_t* census_r, int width,
+               int height, const sva_sgm_params* p, uint8_t* C);
+int sva_paths_d(void* ctx, const uint8_t* C, int width, int height, const sva_sgm_params* p,
+                uint8_t* L8);
+int sva_aggregate_d(void* ctx, const uint8_t* C, int width, int height,
+                    const sva_sgm_params* p, uint16_t* S);
+int sva_wta_d(void* ctx, const uint16_t* S, int width, int height, const sva_sgm_params* p,
+              uint16_t* disp, float* subpix);
+
+/* -------------------------------------------- Mode R (reference parity) --- */
+/* The reference's own path, bit-exact: per pixel the t_near/t_far ray ends
+ * (CameraStereoVision.cpp:60-64, Camera.cpp:15-34), bounds check (:66-71),
+ * Bresenham candidates (functions.cpp:253-321), 2k x 2k SAD (getAbsDiff,
+ * functions.cpp:215-218), first-minimum WTA (:85), (uchar)(int)norm (:89).
+ * mask: W*H u8 or NULL (all selected, :53).  Writes only pixels the pair keeps
+ * (multi-pair callers overwrite in order, :55); disp_u16 / valid nullable. */
+int sva_disparity_ref(void* ctx, const uint8_t* ref_img, const uint8_t* other_img, int width,
+                      int height, size_t pitch, const uint8_t* mask,
+                      const sva_camera* ref_cam, const sva_camera* other_cam, int k,
+                      double t_near, double t_far, uint8_t* disp_u8, uint16_t* disp_u16,
+                      uint8_t* valid);
+int sva_disparity_ref_d(void* ctx, const uint8_t* ref_img, const uint8_t* other_img,
+                        int width, int height, size_t pitch, const uint8_t* mask,
+                        const sva_camera* ref_cam, const sva_camera* other_cam, int k,
+                        double t_near, double t_far, uint8_t* disp_u8, uint16_t* disp_u16,
+                        uint8_t* valid);
+/* Stage: per-pixel ray endpoints (CameraStereoVision.cpp:60-71).
+ * ends: W*H*4 int32 (p1x, p1y, p2x, p2y); valid: W*H u8. */
+int sva_ref_endpoints_d(void* ctx, int width, int height, const sva_camera* ref_cam,
+                        const sva_camera* other_cam, int k, double t_near, double t_far,
+                        int32_t* ends, uint8_t* valid);
+
+/* Disparity -> depth, CameraStereoVision.cpp:47,98-100 (f64; 0 where disp 0). */
+int sva_disparity_to_depth_d(void* ctx, const uint8_t* disp, int n, double cam_distance,
+                             double f, double pixel_size, double* depth);
+
+/* -------------------------------------------------- multi-pair batch --- */
+/* Independent pairs round-robin over the given contexts (one per device),
+ * one host thread per context.  Replaces the `for (auto pair : pairs)` loop
+ * (CameraStereoVision.cpp:55) for whole-image Mode S matching. */
+int sva_batch_sgm(void** ctxs, int n_ctx, const sva_pair_job* jobs, int n_jobs,
+                  const sva_sgm_params* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SVA_H */

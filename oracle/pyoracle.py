@@ -1,0 +1,192 @@
+"""ctypes binding of liboracle.so -- the CPU ORACLE (test infrastructure only).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, and only as the checker or the timed CPU baseline.  Parity status:
+"parity unpinned" (see sva_oracle.h and DESIGN.md §5).
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+class OCamera(ct.Structure):
+    _fields_ = [("f", ct.c_double), ("pos", ct.c_double * 3), ("pixel_size", ct.c_double)]
+
+    @classmethod
+    def make(cls, f, pos, pixel_size):
+        c = cls()
+        c.f = f
+        c.pos[0], c.pos[1], c.pos[2] = pos
+        c.pixel_size = pixel_size
+        return c
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = ct.CDLL(LIB_PATH)
+    vp, i32, dbl, P = ct.c_void_p, ct.c_int, ct.c_double, ct.POINTER
+    sig = {
+        "svo_cam_project": (None, [P(OCamera), P(dbl), P(i32)]),
+        "svo_cam_inv_project": (None, [P(OCamera), i32, i32, P(dbl)]),
+        "svo_bresenham": (i32, [i32, i32, i32, i32, P(i32), P(i32), i32]),
+        "svo_sad": (ct.c_int64, [vp, ct.c_ssize_t, vp, ct.c_ssize_t, i32, i32]),
+        "svo_ref_endpoints": (i32, [P(OCamera), P(OCamera), i32, i32, i32, dbl, dbl, i32, i32,
+                                    P(i32), P(i32)]),
+        "svo_ref_pair": (ct.c_int64, [vp, vp, i32, i32, ct.c_ssize_t, vp, P(OCamera), P(OCamera),
+                                      i32, dbl, dbl, vp, vp, vp]),
+        "svo_disp_to_depth": (None, [vp, i32, dbl, dbl, dbl, vp]),
+        "svo_census": (None, [vp, i32, i32, ct.c_ssize_t, vp]),
+        "svo_cost": (None, [vp, vp, i32, i32, i32, i32, i32, vp]),
+        "svo_path": (None, [vp, i32, i32, i32, i32, i32, i32, i32, vp]),
+        "svo_direction": (None, [i32, P(i32), P(i32)]),
+        "svo_aggregate": (None, [vp, i32, i32, i32, i32, i32, vp, i32]),
+        "svo_wta": (None, [vp, i32, i32, i32, i32, vp, vp]),
+        "svo_sgm": (None, [vp, vp, i32, i32, ct.c_ssize_t, i32, i32, i32, i32, i32, vp, vp, i32]),
+        "svo_lr_check": (None, [vp, vp, i32, i32, i32, i32, ct.c_uint16]),
+    }
+    for n, (r, a) in sig.items():
+        f = getattr(lib, n)
+        f.restype = r
+        f.argtypes = a
+    return lib
+
+
+lib = _load()
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+# ------------------------------------------------------------------ Mode R --
+def project(cam: OCamera, P):
+    out = (ct.c_int * 2)()
+    lib.svo_cam_project(ct.byref(cam), (ct.c_double * 3)(*P), out)
+    return out[0], out[1]
+
+
+def inv_project(cam: OCamera, px: int, py: int):
+    out = (ct.c_double * 3)()
+    lib.svo_cam_inv_project(ct.byref(cam), px, py, out)
+    return out[0], out[1], out[2]
+
+
+def bresenham(p1, p2):
+    cap = 4 * (abs(p1[0] - p2[0]) + abs(p1[1] - p2[1])) + 8
+    xs = (ct.c_int * cap)()
+    ys = (ct.c_int * cap)()
+    n = lib.svo_bresenham(p1[0], p1[1], p2[0], p2[1], xs, ys, cap)
+    return [(xs[i], ys[i]) for i in range(n)]
+
+
+def ref_endpoints(cref, coth, W, H, k, t_near, t_far, x, y):
+    a = (ct.c_int * 2)()
+    b = (ct.c_int * 2)()
+    ok = lib.svo_ref_endpoints(ct.byref(cref), ct.byref(coth), W, H, k, t_near, t_far, x, y, a, b)
+    return bool(ok), (a[0], a[1]), (b[0], b[1])
+
+
+def ref_pair(ref, other, cref, coth, k=20, t_near=0.5, t_far=1.0, mask=None,
+             disp_u8=None, disp_u16=None, valid=None):
+    ref = _c(ref, np.uint8)
+    other = _c(other, np.uint8)
+    H, W = ref.shape
+    disp_u8 = np.zeros((H, W), np.uint8) if disp_u8 is None else disp_u8
+    disp_u16 = np.zeros((H, W), np.uint16) if disp_u16 is None else disp_u16
+    valid = np.zeros((H, W), np.uint8) if valid is None else valid
+    m = None if mask is None else _c(mask, np.uint8)
+    n = lib.svo_ref_pair(_p(ref), _p(other), W, H, W, _p(m), ct.byref(cref), ct.byref(coth), k,
+                         t_near, t_far, _p(disp_u8), _p(disp_u16), _p(valid))
+    return disp_u8, disp_u16, valid, n
+
+
+def disp_to_depth(disp, cam_distance, f, pixel_size):
+    d = _c(disp, np.uint8)
+    out = np.zeros(d.shape, np.float64)
+    lib.svo_disp_to_depth(_p(d), d.size, cam_distance, f, pixel_size, _p(out))
+    return out
+
+
+# ------------------------------------------------------------------ Mode S --
+def census(img):
+    img = _c(img, np.uint8)
+    H, W = img.shape
+    out = np.zeros((H, W), np.uint64)
+    lib.svo_census(_p(img), W, H, W, _p(out))
+    return out
+
+
+def cost(cl, cr, D, dmin, dir):
+    cl = _c(cl, np.uint64)
+    cr = _c(cr, np.uint64)
+    H, W = cl.shape
+    C = np.zeros((H, W, D), np.uint8)
+    lib.svo_cost(_p(cl), _p(cr), W, H, D, dmin, dir, _p(C))
+    return C
+
+
+def direction(r):
+    rx, ry = ct.c_int(), ct.c_int()
+    lib.svo_direction(r, ct.byref(rx), ct.byref(ry))
+    return rx.value, ry.value
+
+
+def path(C, r, P1=10, P2=120):
+    C = _c(C, np.uint8)
+    H, W, D = C.shape
+    rx, ry = direction(r)
+    L = np.zeros_like(C)
+    lib.svo_path(_p(C), W, H, D, rx, ry, P1, P2, _p(L))
+    return L
+
+
+def aggregate(C, P1=10, P2=120, threads=1):
+    C = _c(C, np.uint8)
+    H, W, D = C.shape
+    S = np.zeros((H, W, D), np.uint16)
+    lib.svo_aggregate(_p(C), W, H, D, P1, P2, _p(S), threads)
+    return S
+
+
+def wta(S, dmin=0, subpixel=True):
+    S = _c(S, np.uint16)
+    H, W, D = S.shape
+    disp = np.zeros((H, W), np.uint16)
+    sub = np.zeros((H, W), np.float32) if subpixel else None
+    lib.svo_wta(_p(S), W, H, D, dmin, _p(disp), _p(sub))
+    return disp, sub
+
+
+def sgm(left, right, D, dmin=0, dir=-1, P1=10, P2=120, subpixel=True, threads=1):
+    left = _c(left, np.uint8)
+    right = _c(right, np.uint8)
+    H, W = left.shape
+    disp = np.zeros((H, W), np.uint16)
+    sub = np.zeros((H, W), np.float32) if subpixel else None
+    lib.svo_sgm(_p(left), _p(right), W, H, W, D, dmin, dir, P1, P2, _p(disp), _p(sub), threads)
+    return disp, sub
+
+
+def lr_check(disp_l, disp_r, dir, max_diff=1, invalid=0xFFFF):
+    dl = _c(disp_l, np.uint16).copy()
+    dr = _c(disp_r, np.uint16)
+    H, W = dl.shape
+    lib.svo_lr_check(_p(dl), _p(dr), W, H, dir, max_diff, invalid)
+    return dl

@@ -1,0 +1,231 @@
+/*
+ * sgm_oracle.c -- CPU ORACLE, Mode S (Census 9x7 -> Hamming cost volume ->
+ * 8-path SGM -> winner-take-all + sub-pixel).
+ * TEST INFRASTRUCTURE ONLY (see sva_oracle.h).
+ *
+ * The reference has no Census/Hamming/SGM, so this file follows
+ * the frozen spec in DESIGN.md §2.  The WTA
+ * tie-break (first minimum in index order) mirrors the reference's
+ * std::min_element at src/CameraStereoVision.cpp:85.  Parity unpinned.
+ *
+ * Written for clarity, not speed: plain int arithmetic, one direction at a
+ * time.  The optional OpenMP threads only split independent path lines.
+ */
+#include "sva_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* DESIGN.md §2.1 -- census 9 wide x 7 high. */
+void svo_census(const uint8_t* img, int W, int H, ptrdiff_t pitch, uint64_t* out) {
+    for (int y = 0; y < H; y++) {
+        for (int x = 0; x < W; x++) {
+            uint64_t w = 0;
+            if (x >= 4 && x < W - 4 && y >= 3 && y < H - 3) {
+                int c = img[(ptrdiff_t)y * pitch + x];
+                for (int dy = -3; dy <= 3; dy++)
+                    for (int dx = -4; dx <= 4; dx++) {
+                        if (dx == 0 && dy == 0) continue;
+                        int q = img[(ptrdiff_t)(y + dy) * pitch + (x + dx)];
+                        w = (w << 1) | (uint64_t)(q < c);
+                    }
+            }
+            out[(size_t)y * W + x] = w;
+        }
+    }
+}
+
+static int popcount64(uint64_t v) {
+    int n = 0;
+    while (v) { v &= v - 1; n++; }
+    return n;
+}
+
+/* DESIGN.md §2.2 -- Hamming matching cost, D-contiguous u8. */
+void svo_cost(const uint64_t* cl, const uint64_t* cr, int W, int H, int D, int dmin, int dir,
+              uint8_t* C) {
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++)
+            for (int d = 0; d < D; d++) {
+                int xr = x + dir * (dmin + d);
+                int c = 62;
+                if (xr >= 0 && xr < W)
+                    c = popcount64(cl[(size_t)y * W + x] ^ cr[(size_t)y * W + xr]);
+                C[((size_t)y * W + x) * D + d] = (uint8_t)c;
+            }
+}
+
+/* DESIGN.md §2.3 -- direction table r = 0..7 (step vectors p = q + r). */
+void svo_direction(int r, int* rx, int* ry) {
+    static const int T[8][2] = {{1, 0}, {-1, 0}, {0, 1}, {0, -1},
+                                {1, 1}, {-1, -1}, {-1, 1}, {1, -1}};
+    *rx = T[r & 7][0];
+    *ry = T[r & 7][1];
+}
+
+/* L_r(p,d) = C(p,d) + min(L(q,d), L(q,d-1)+P1, L(q,d+1)+P1, m+P2) - m,
+ * m = min_k L(q,k), q = p - r; L = C where q is outside the image.
+ * Visiting order: rows in the direction of ry (top-down if ry >= 0), columns
+ * in the direction of rx, so q is always finished before p.                 */
+void svo_path(const uint8_t* C, int W, int H, int D, int rx, int ry, int P1, int P2,
+              uint8_t* L) {
+    for (int yi = 0; yi < H; yi++) {
+        int y = ry >= 0 ? yi : H - 1 - yi;
+        for (int xi = 0; xi < W; xi++) {
+            int x = rx >= 0 ? xi : W - 1 - xi;
+            const uint8_t* c = C + ((size_t)y * W + x) * D;
+            uint8_t* l = L + ((size_t)y * W + x) * D;
+            int qx = x - rx, qy = y - ry;
+            if (qx < 0 || qx >= W || qy < 0 || qy >= H) {
+                memcpy(l, c, (size_t)D);
+                continue;
+            }
+            const uint8_t* lq = L + ((size_t)qy * W + qx) * D;
+            int m = lq[0];
+            for (int k = 1; k < D; k++) if (lq[k] < m) m = lq[k];
+            for (int d = 0; d < D; d++) {
+                int best = lq[d];
+                if (d > 0 && lq[d - 1] + P1 < best) best = lq[d - 1] + P1;
+                if (d < D - 1 && lq[d + 1] + P1 < best) best = lq[d + 1] + P1;
+                if (m + P2 < best) best = m + P2;
+                l[d] = (uint8_t)(c[d] + best - m);
+            }
+        }
+    }
+}
+
+void svo_aggregate(const uint8_t* C, int W, int H, int D, int P1, int P2, uint16_t* S,
+                   int threads) {
+    size_t n = (size_t)W * H * D;
+    memset(S, 0, n * sizeof(uint16_t));
+    uint8_t* L = (uint8_t*)malloc(n);
+    for (int r = 0; r < 8; r++) {
+        int rx, ry;
+        svo_direction(r, &rx, &ry);
+        svo_path(C, W, H, D, rx, ry, P1, P2, L);
+        (void)threads;
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(threads > 1 ? threads : 1) schedule(static)
+#endif
+        for (long long i = 0; i < (long long)n; i++) S[i] = (uint16_t)(S[i] + L[i]);
+    }
+    free(L);
+}
+
+/* DESIGN.md §2.4 -- first-minimum WTA (mirrors CameraStereoVision.cpp:85)
+ * and parabola sub-pixel in f32. */
+void svo_wta(const uint16_t* S, int W, int H, int D, int dmin, uint16_t* disp, float* sub) {
+    for (size_t p = 0; p < (size_t)W * H; p++) {
+        const uint16_t* s = S + p * D;
+        int best = 0;
+        for (int d = 1; d < D; d++) if (s[d] < s[best]) best = d;
+        disp[p] = (uint16_t)(dmin + best);
+        if (sub) {
+            float v = (float)(dmin + best);
+            if (best > 0 && best < D - 1) {
+                int a = s[best - 1], b = s[best], c = s[best + 1];
+                int den = a - 2 * b + c;
+                if (den > 0) v = v + (float)(a - c) / (float)(2 * den);
+            }
+            sub[p] = v;
+        }
+    }
+}
+
+/* Path-parallel variant of svo_path used only to speed up the CPU baseline:
+ * lines of one direction are independent, so the image is split into the
+ * lines the direction sweeps.  Same arithmetic as svo_path. */
+static void path_line_step(const uint8_t* C, uint8_t* L, int W, int H, int D, int x, int y,
+                           int rx, int ry, int P1, int P2) {
+    const uint8_t* c = C + ((size_t)y * W + x) * D;
+    uint8_t* l = L + ((size_t)y * W + x) * D;
+    int qx = x - rx, qy = y - ry;
+    if (qx < 0 || qx >= W || qy < 0 || qy >= H) {
+        memcpy(l, c, (size_t)D);
+        return;
+    }
+    const uint8_t* lq = L + ((size_t)qy * W + qx) * D;
+    int m = lq[0];
+    for (int k = 1; k < D; k++) if (lq[k] < m) m = lq[k];
+    for (int d = 0; d < D; d++) {
+        int best = lq[d];
+        if (d > 0 && lq[d - 1] + P1 < best) best = lq[d - 1] + P1;
+        if (d < D - 1 && lq[d + 1] + P1 < best) best = lq[d + 1] + P1;
+        if (m + P2 < best) best = m + P2;
+        l[d] = (uint8_t)(c[d] + best - m);
+    }
+}
+
+static void svo_path_threaded(const uint8_t* C, int W, int H, int D, int rx, int ry, int P1,
+                              int P2, uint8_t* L, int threads) {
+    if (ry == 0) {
+        /* horizontal: rows independent */
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(threads) schedule(static)
+#endif
+        for (int y = 0; y < H; y++)
+            for (int xi = 0; xi < W; xi++)
+                path_line_step(C, L, W, H, D, rx > 0 ? xi : W - 1 - xi, y, rx, ry, P1, P2);
+    } else {
+        /* vertical / diagonal: a row depends only on the previous row */
+        for (int yi = 0; yi < H; yi++) {
+            int y = ry > 0 ? yi : H - 1 - yi;
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(threads) schedule(static)
+#endif
+            for (int x = 0; x < W; x++) path_line_step(C, L, W, H, D, x, y, rx, ry, P1, P2);
+        }
+    }
+}
+
+void svo_sgm(const uint8_t* left, const uint8_t* right, int W, int H, ptrdiff_t pitch, int D,
+             int dmin, int dir, int P1, int P2, uint16_t* disp, float* sub, int threads) {
+    size_t np = (size_t)W * H, n = np * D;
+    uint64_t* cl = (uint64_t*)malloc(np * 8);
+    uint64_t* cr = (uint64_t*)malloc(np * 8);
+    uint8_t* C = (uint8_t*)malloc(n);
+    uint16_t* S = (uint16_t*)malloc(n * 2);
+    svo_census(left, W, H, pitch, cl);
+    svo_census(right, W, H, pitch, cr);
+    svo_cost(cl, cr, W, H, D, dmin, dir, C);
+    if (threads > 1) {
+        uint8_t* L = (uint8_t*)malloc(n);
+        memset(S, 0, n * 2);
+        for (int r = 0; r < 8; r++) {
+            int rx, ry;
+            svo_direction(r, &rx, &ry);
+            svo_path_threaded(C, W, H, D, rx, ry, P1, P2, L, threads);
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(threads) schedule(static)
+#endif
+            for (long long i = 0; i < (long long)n; i++) S[i] = (uint16_t)(S[i] + L[i]);
+        }
+        free(L);
+    } else {
+        svo_aggregate(C, W, H, D, P1, P2, S, 1);
+    }
+    svo_wta(S, W, H, D, dmin, disp, sub);
+    free(cl);
+    free(cr);
+    free(C);
+    free(S);
+}
+
+/* DESIGN.md §2.5 -- left/right consistency. */
+void svo_lr_check(uint16_t* disp_l, const uint16_t* disp_r, int W, int H, int dir,
+                  int max_diff, uint16_t invalid) {
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            uint16_t* dl = disp_l + (size_t)y * W + x;
+            if (*dl == invalid) continue;
+            int xr = x + dir * (int)*dl;
+            if (xr < 0 || xr >= W) { *dl = invalid; continue; }
+            int dr = disp_r[(size_t)y * W + xr];
+            int diff = (int)*dl - dr;
+            if (diff < 0) diff = -diff;
+            if (dr == invalid || diff > max_diff) *dl = invalid;
+        }
+}

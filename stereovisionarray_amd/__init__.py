@@ -1,0 +1,289 @@
+"""stereovisionarray_amd -- MI355X-native stereo disparity engine.
+
+The product is the C-ABI shared library ``libsva.so`` (hand-written HIP
+kernels for gfx950 + a C++ host layer, declared in ``include/sva.h``).  This
+module is a thin ctypes binding used by the tests and ``bench.py``; it adds no
+compute of its own and has no CPU fallback: if ``libsva.so`` is missing, import
+fails loudly, and if no GPU is present every compute call raises.
+
+Host-pointer calls take numpy arrays; ``*_d`` calls take device pointers
+(ints), e.g. ``torch_tensor.data_ptr()``.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsva.so")
+
+SVA_OK = 0
+SVA_ERR_INVALID_ARG = 1
+SVA_ERR_UNSUPPORTED = 2
+SVA_ERR_DEVICE = 3
+SVA_ERR_OUT_OF_MEMORY = 4
+SVA_ERR_NO_DEVICE = 5
+
+# Symbols declared in include/sva.h (checked by tests/test_abi.py).
+EXPORTED = [
+    "sva_sgm_params_default", "sva_abi_version", "sva_device_count", "sva_create",
+    "sva_destroy", "sva_set_stream", "sva_synchronize", "sva_last_error",
+    "sva_status_string", "sva_reserve", "sva_set_timing", "sva_reset_timing",
+    "sva_kernel_time", "sva_disparity_sgm", "sva_disparity_sgm_d", "sva_census_d",
+    "sva_cost_d", "sva_paths_d", "sva_aggregate_d", "sva_wta_d", "sva_disparity_ref",
+    "sva_disparity_ref_d", "sva_ref_endpoints_d", "sva_disparity_to_depth_d",
+    "sva_batch_sgm",
+]
+
+
+class SgmParams(ct.Structure):
+    """Mirror of ``sva_sgm_params`` (include/sva.h)."""
+    _fields_ = [
+        ("D", ct.c_int32), ("dmin", ct.c_int32), ("dir", ct.c_int32),
+        ("P1", ct.c_int32), ("P2", ct.c_int32), ("subpixel", ct.c_int32),
+        ("lr_check", ct.c_int32), ("lr_max_diff", ct.c_int32),
+        ("invalid", ct.c_uint16), ("_pad", ct.c_uint16),
+    ]
+
+
+class Camera(ct.Structure):
+    """Mirror of ``sva_camera`` = class Camera (include/Camera.h:6-21)."""
+    _fields_ = [("f", ct.c_double), ("pos", ct.c_double * 3), ("pixel_size", ct.c_double)]
+
+    @classmethod
+    def make(cls, f, pos, pixel_size):
+        c = cls()
+        c.f = f
+        c.pos[0], c.pos[1], c.pos[2] = pos
+        c.pixel_size = pixel_size
+        return c
+
+
+class PairJob(ct.Structure):
+    _fields_ = [
+        ("left", ct.c_void_p), ("right", ct.c_void_p), ("width", ct.c_int32),
+        ("height", ct.c_int32), ("pitch", ct.c_size_t), ("disp", ct.c_void_p),
+        ("subpix", ct.c_void_p),
+    ]
+
+
+class SvaError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"sva status {status}: {msg}")
+        self.status = status
+
+
+def _load() -> ct.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback)")
+    lib = ct.CDLL(LIB_PATH)
+    vp, i32, sz, dbl = ct.c_void_p, ct.c_int, ct.c_size_t, ct.c_double
+    P = ct.POINTER
+    sig = {
+        "sva_sgm_params_default": (None, [P(SgmParams)]),
+        "sva_abi_version": (i32, []),
+        "sva_device_count": (i32, [P(i32)]),
+        "sva_create": (i32, [i32, P(vp)]),
+        "sva_destroy": (i32, [vp]),
+        "sva_set_stream": (i32, [vp, vp]),
+        "sva_synchronize": (i32, [vp]),
+        "sva_last_error": (ct.c_char_p, [vp]),
+        "sva_status_string": (ct.c_char_p, [i32]),
+        "sva_reserve": (i32, [vp, i32, i32, i32]),
+        "sva_set_timing": (i32, [vp, i32]),
+        "sva_reset_timing": (i32, [vp]),
+        "sva_kernel_time": (i32, [vp, ct.c_char_p, P(dbl), P(ct.c_int64)]),
+        "sva_disparity_sgm": (i32, [vp, vp, vp, i32, i32, sz, P(SgmParams), vp, vp]),
+        "sva_disparity_sgm_d": (i32, [vp, vp, vp, i32, i32, sz, P(SgmParams), vp, vp]),
+        "sva_census_d": (i32, [vp, vp, i32, i32, sz, vp]),
+        "sva_cost_d": (i32, [vp, vp, vp, i32, i32, P(SgmParams), vp]),
+        "sva_paths_d": (i32, [vp, vp, i32, i32, P(SgmParams), vp]),
+        "sva_aggregate_d": (i32, [vp, vp, i32, i32, P(SgmParams), vp]),
+        "sva_wta_d": (i32, [vp, vp, i32, i32, P(SgmParams), vp, vp]),
+        "sva_disparity_ref": (i32, [vp, vp, vp, i32, i32, sz, vp, P(Camera), P(Camera), i32,
+                                    dbl, dbl, vp, vp, vp]),
+        "sva_disparity_ref_d": (i32, [vp, vp, vp, i32, i32, sz, vp, P(Camera), P(Camera), i32,
+                                      dbl, dbl, vp, vp, vp]),
+        "sva_ref_endpoints_d": (i32, [vp, i32, i32, P(Camera), P(Camera), i32, dbl, dbl, vp, vp]),
+        "sva_disparity_to_depth_d": (i32, [vp, vp, i32, dbl, dbl, dbl, vp]),
+        "sva_batch_sgm": (i32, [P(vp), i32, P(PairJob), i32, P(SgmParams)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def default_params(**kw) -> SgmParams:
+    p = SgmParams()
+    lib.sva_sgm_params_default(ct.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def device_count() -> int:
+    n = ct.c_int(0)
+    lib.sva_device_count(ct.byref(n))
+    return n.value
+
+
+def _ptr(a) -> int | None:
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return a
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()  # torch tensor
+
+
+class Context:
+    """One device + one stream (``sva_create``)."""
+
+    def __init__(self, device: int = 0):
+        h = ct.c_void_p()
+        st = lib.sva_create(device, ct.byref(h))
+        if st != SVA_OK:
+            raise SvaError(st, lib.sva_status_string(st).decode())
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib.sva_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _chk(self, st: int):
+        if st != SVA_OK:
+            raise SvaError(st, lib.sva_last_error(self.h).decode())
+
+    # -- plumbing
+    def set_stream(self, stream_ptr: int | None):
+        self._chk(lib.sva_set_stream(self.h, stream_ptr))
+
+    def synchronize(self):
+        self._chk(lib.sva_synchronize(self.h))
+
+    def reserve(self, W, H, D):
+        self._chk(lib.sva_reserve(self.h, W, H, D))
+
+    def set_timing(self, on: bool):
+        self._chk(lib.sva_set_timing(self.h, 1 if on else 0))
+
+    def reset_timing(self):
+        self._chk(lib.sva_reset_timing(self.h))
+
+    def kernel_time(self, name: str) -> tuple[float, int]:
+        ms = ct.c_double(0)
+        n = ct.c_int64(0)
+        self._chk(lib.sva_kernel_time(self.h, name.encode(), ct.byref(ms), ct.byref(n)))
+        return ms.value, n.value
+
+    # -- Mode S, host arrays
+    def disparity_sgm(self, left: np.ndarray, right: np.ndarray, params: SgmParams):
+        assert left.dtype == np.uint8 and right.dtype == np.uint8 and left.shape == right.shape
+        left = np.ascontiguousarray(left)
+        right = np.ascontiguousarray(right)
+        H, W = left.shape
+        disp = np.zeros((H, W), np.uint16)
+        sub = np.zeros((H, W), np.float32) if params.subpixel else None
+        self._chk(lib.sva_disparity_sgm(self.h, _ptr(left), _ptr(right), W, H, W,
+                                        ct.byref(params), _ptr(disp), _ptr(sub)))
+        return disp, sub
+
+    # -- Mode S, device pointers (async on the context stream)
+    def disparity_sgm_d(self, left, right, W, H, pitch, params, disp, sub=None):
+        self._chk(lib.sva_disparity_sgm_d(self.h, _ptr(left), _ptr(right), W, H, pitch,
+                                          ct.byref(params), _ptr(disp), _ptr(sub)))
+
+    def census_d(self, img, W, H, pitch, out):
+        self._chk(lib.sva_census_d(self.h, _ptr(img), W, H, pitch, _ptr(out)))
+
+    def cost_d(self, cl, cr, W, H, params, C):
+        self._chk(lib.sva_cost_d(self.h, _ptr(cl), _ptr(cr), W, H, ct.byref(params), _ptr(C)))
+
+    def paths_d(self, C, W, H, params, L8):
+        self._chk(lib.sva_paths_d(self.h, _ptr(C), W, H, ct.byref(params), _ptr(L8)))
+
+    def aggregate_d(self, C, W, H, params, S):
+        self._chk(lib.sva_aggregate_d(self.h, _ptr(C), W, H, ct.byref(params), _ptr(S)))
+
+    def wta_d(self, S, W, H, params, disp, sub=None):
+        self._chk(lib.sva_wta_d(self.h, _ptr(S), W, H, ct.byref(params), _ptr(disp), _ptr(sub)))
+
+    # -- Mode R
+    def disparity_ref(self, ref: np.ndarray, other: np.ndarray, cref: Camera, coth: Camera,
+                      k: int = 20, t_near: float = 0.5, t_far: float = 1.0, mask=None,
+                      disp_u8=None, disp_u16=None, valid=None):
+        ref = np.ascontiguousarray(ref)
+        other = np.ascontiguousarray(other)
+        H, W = ref.shape
+        if disp_u8 is None:
+            disp_u8 = np.zeros((H, W), np.uint8)
+        if disp_u16 is None:
+            disp_u16 = np.zeros((H, W), np.uint16)
+        if valid is None:
+            valid = np.zeros((H, W), np.uint8)
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        self._chk(lib.sva_disparity_ref(self.h, _ptr(ref), _ptr(other), W, H, W, _ptr(m),
+                                        ct.byref(cref), ct.byref(coth), k, t_near, t_far,
+                                        _ptr(disp_u8), _ptr(disp_u16), _ptr(valid)))
+        return disp_u8, disp_u16, valid
+
+    def disparity_ref_d(self, ref, other, W, H, pitch, mask, cref, coth, k, t_near, t_far,
+                        disp_u8, disp_u16=None, valid=None):
+        self._chk(lib.sva_disparity_ref_d(self.h, _ptr(ref), _ptr(other), W, H, pitch, _ptr(mask),
+                                          ct.byref(cref), ct.byref(coth), k, t_near, t_far,
+                                          _ptr(disp_u8), _ptr(disp_u16), _ptr(valid)))
+
+    def ref_endpoints_d(self, W, H, cref, coth, k, t_near, t_far, ends, valid):
+        self._chk(lib.sva_ref_endpoints_d(self.h, W, H, ct.byref(cref), ct.byref(coth), k,
+                                          t_near, t_far, _ptr(ends), _ptr(valid)))
+
+    def disparity_to_depth_d(self, disp, n, cam_distance, f, pixel_size, depth):
+        self._chk(lib.sva_disparity_to_depth_d(self.h, _ptr(disp), n, cam_distance, f,
+                                               pixel_size, _ptr(depth)))
+
+
+def batch_sgm(contexts: list[Context], pairs: list[tuple[np.ndarray, np.ndarray]],
+              params: SgmParams):
+    """Match independent pairs round-robin over ``contexts`` (``sva_batch_sgm``)."""
+    jobs = (PairJob * len(pairs))()
+    outs = []
+    keep = []
+    for i, (l, r) in enumerate(pairs):
+        l = np.ascontiguousarray(l)
+        r = np.ascontiguousarray(r)
+        H, W = l.shape
+        d = np.zeros((H, W), np.uint16)
+        s = np.zeros((H, W), np.float32) if params.subpixel else None
+        keep += [l, r]
+        outs.append((d, s))
+        jobs[i] = PairJob(_ptr(l), _ptr(r), W, H, W, _ptr(d), _ptr(s))
+    hs = (ct.c_void_p * len(contexts))(*[c.h.value for c in contexts])
+    st = lib.sva_batch_sgm(hs, len(contexts), jobs, len(pairs), ct.byref(params))
+    if st != SVA_OK:
+        raise SvaError(st, lib.sva_status_string(st).decode())
+    return outs

@@ -1,0 +1,257 @@
+// refpath.hip -- Mode R: the reference's own disparity path, bit-exact
+// (DESIGN.md §3).
+//
+//   ref_endpoints_kernel  one thread per pixel, IEEE f64 in the reference's
+//                         operand order (Camera.cpp:15-34,
+//                         CameraStereoVision.cpp:28,60-71).  FMA contraction
+//                         is off for this file so every rounding matches.
+//   ref_match_kernel      one wave per pixel, one lane per Bresenham
+//                         candidate (functions.cpp:253-321 in closed form),
+//                         2k x 2k SAD with v_sad_u8 (4 |a-b| per lane-op) on
+//                         dword-realigned rows (v_alignbyte), first-minimum
+//                         argmin as a wave-wide u64 min over (SAD << 32 | i),
+//                         then (uchar)(int)sqrt(dx^2 + dy^2)
+//                         (CameraStereoVision.cpp:85-89).
+#pragma clang fp contract(off)
+
+#include "sva_device.h"
+#include "sva_internal.h"
+
+namespace sva {
+namespace {
+
+struct CamD {
+    double f, px, py, pz, ps;
+};
+
+__device__ __forceinline__ CamD cam_of(const sva_camera& c) {
+    return CamD{c.f, c.pos[0], c.pos[1], c.pos[2], c.pixel_size};
+}
+
+// Camera::project (Camera.cpp:15-21)
+__device__ __forceinline__ void project(const CamD& c, double X, double Y, double Z, int& u,
+                                        int& v) {
+    const double mult = c.f / (Z - c.pz) / c.ps;
+    u = (int)((X - c.px) * mult);
+    v = (int)((Y - c.py) * mult);
+}
+
+__global__ void ref_endpoints_kernel(int W, int H, sva_camera cref_, sva_camera coth_, int k,
+                                     double t_near, double t_far, int4* __restrict__ ends,
+                                     uint8_t* __restrict__ valid) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= W) return;
+    const size_t p = (size_t)y * W + x;
+    const CamD cr = cam_of(cref_), co = cam_of(coth_);
+    const int hx = W / 2, hy = H / 2;  // halfRes = resolution / 2 (:28)
+    // Camera::inv_project (Camera.cpp:25-33): vector / norm(vector)
+    const double v0 = (double)(x - hx) * cr.ps;
+    const double v1 = (double)(y - hy) * cr.ps;
+    const double v2 = cr.f;
+    const double n = __builtin_sqrt(v0 * v0 + v1 * v1 + v2 * v2);
+    const double e0 = v0 / n, e1 = v1 / n, e2 = v2 / n;
+    // p1 = pos3D + vec*t_near ; p2 = pos3D + vec*t_far (:61-62)
+    int a0, a1, b0, b1;
+    project(co, cr.px + e0 * t_near, cr.py + e1 * t_near, cr.pz + e2 * t_near, a0, a1);
+    project(co, cr.px + e0 * t_far, cr.py + e1 * t_far, cr.pz + e2 * t_far, b0, b1);
+    a0 += hx; a1 += hy; b0 += hx; b1 += hy;
+    bool ok = x >= k && x < W - k && y >= k && y < H - k;   // loop bounds (:49,51)
+    ok = ok && !(a0 < k || a1 < k || a0 > W - k || a1 > H - k);  // :66
+    ok = ok && !(b0 < k || b1 < k || b0 > W - k || b1 > H - k);  // :69
+    ends[p] = make_int4(a0, a1, b0, b1);
+    valid[p] = ok ? 1 : 0;
+}
+
+// Closed form of functions.cpp:253-321.  The line is stored as its start
+// point, the major-axis direction and the Bresenham slope numerator/denominator
+// so candidate i is O(1):  plotLineLow emits (x0+i, y0 + yi*floor((2|dy|i + dx - 1) / (2dx))),
+// plotLineHigh the transpose.  (Proof: the error term D_i = 2|dy|(i+1) - dx -
+// 2dx*n_i stays in (-2dx, 2|dy|], which gives n_i = ceil((2|dy|i - dx)/(2dx)).)
+struct Line {
+    int x0, y0;   // first emitted point
+    int high;     // 1: plotLineHigh (y major)
+    int step;     // +-1 minor-axis step (yi / xi)
+    int a, b;     // 2*|minor delta|, 2*major delta
+    int major;    // major delta (dx for low, dy for high)
+    int n;        // number of points
+};
+
+__device__ __forceinline__ Line make_line(int p1x, int p1y, int p2x, int p2y) {
+    // bresenham(point2 = pixel1, point1 = pixel2), functions.cpp:299-321
+    const int ax = p1x, ay = p1y, bx = p2x, by = p2y;
+    int x0, y0, x1, y1;
+    Line L;
+    if (abs(ay - by) < abs(ax - bx)) {
+        if (bx > ax) { x0 = ax; y0 = ay; x1 = bx; y1 = by; }
+        else { x0 = bx; y0 = by; x1 = ax; y1 = ay; }
+        int dx = x1 - x0, dy = y1 - y0;
+        L.high = 0;
+        L.step = dy < 0 ? -1 : 1;
+        L.a = 2 * (dy < 0 ? -dy : dy);
+        L.b = 2 * dx;
+        L.major = dx;
+        L.n = dx + 1;
+    } else {
+        if (by > ay) { x0 = ax; y0 = ay; x1 = bx; y1 = by; }
+        else { x0 = bx; y0 = by; x1 = ax; y1 = ay; }
+        int dx = x1 - x0, dy = y1 - y0;
+        L.high = 1;
+        L.step = dx < 0 ? -1 : 1;
+        L.a = 2 * (dx < 0 ? -dx : dx);
+        L.b = 2 * dy;
+        L.major = dy;
+        L.n = dy + 1;   // dy >= 0 here; dy == 0 only for a single point
+    }
+    L.x0 = x0;
+    L.y0 = y0;
+    return L;
+}
+
+__device__ __forceinline__ void line_point(const Line& L, int i, int& cx, int& cy) {
+    const int minor = L.b > 0 ? (L.a * i + L.major - 1) / L.b : 0;
+    if (L.high) { cx = L.x0 + L.step * minor; cy = L.y0 + i; }
+    else { cx = L.x0 + i; cy = L.y0 + L.step * minor; }
+}
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
+        unsigned olo = __shfl_xor(lo, off, 64), ohi = __shfl_xor(hi, off, 64);
+        unsigned long long o = ((unsigned long long)ohi << 32) | olo;
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+// Sum |a-b| over one 2k-byte row pair.  ND = ceil(2k/4) dwords; `lastmask`
+// keeps the valid bytes of the final dword (0xffff when 2k % 4 == 2).
+template <int ND>
+__device__ __forceinline__ unsigned sad_row(const uint8_t* a, const uint8_t* b, unsigned lastmask,
+                                            int nbytes, unsigned acc) {
+    const uintptr_t ua = (uintptr_t)a, ub = (uintptr_t)b;
+    const unsigned* wa = (const unsigned*)(ua & ~(uintptr_t)3);
+    const unsigned* wb = (const unsigned*)(ub & ~(uintptr_t)3);
+    const unsigned sa = (unsigned)(ua & 3), sb = (unsigned)(ub & 3);
+    // Never touch a dword past the one holding the last valid byte.
+    const int la = (int)(((ua + nbytes - 1) & ~(uintptr_t)3) - (ua & ~(uintptr_t)3)) >> 2;
+    const int lb = (int)(((ub + nbytes - 1) & ~(uintptr_t)3) - (ub & ~(uintptr_t)3)) >> 2;
+    unsigned ra[ND + 1], rb[ND + 1];
+#pragma unroll
+    for (int j = 0; j <= ND; j++) {
+        ra[j] = wa[j < la ? j : la];
+        rb[j] = wb[j < lb ? j : lb];
+    }
+#pragma unroll
+    for (int j = 0; j < ND; j++) {
+        unsigned oa = __builtin_amdgcn_alignbyte(ra[j + 1], ra[j], sa);
+        unsigned ob = __builtin_amdgcn_alignbyte(rb[j + 1], rb[j], sb);
+        if (j == ND - 1) { oa &= lastmask; ob &= lastmask; }
+        acc = __builtin_amdgcn_sad_u8(oa, ob, acc);
+    }
+    return acc;
+}
+
+template <int ND>
+__global__ __launch_bounds__(256) void ref_match_kernel(
+    const uint8_t* __restrict__ ref, const uint8_t* __restrict__ other, int W, int H, size_t pitch,
+    const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
+    const uint8_t* __restrict__ valid_in, int k, uint8_t* __restrict__ disp_u8,
+    uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out) {
+    const int lane = threadIdx.x & 63;
+    // one wave per pixel of the loop region [k, W-k) x [k, H-k)
+    const int iw = W - 2 * k;
+    const long long q = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    if (q >= (long long)iw * (H - 2 * k)) return;
+    const int y = k + (int)(q / iw), x = k + (int)(q % iw);
+    const size_t p = (size_t)y * W + x;
+    if (!valid_in[p]) return;
+    if (mask && mask[p] == 0) return;                                 // :53
+    const int4 e = ends[p];
+    const Line L = make_line(e.x, e.y, e.z, e.w);                     // :73
+    const int nbytes = 2 * k;
+    const unsigned lastmask = (nbytes & 3) ? 0xffffu : 0xffffffffu;
+    const uint8_t* kern = ref + (size_t)(y - k) * pitch + (x - k);    // :57
+    unsigned long long best = ~0ull;
+    for (int base = 0; base < L.n; base += 64) {                      // :76-83
+        const int i = base + lane;
+        unsigned long long key = ~0ull;
+        if (i < L.n) {
+            int cx, cy;
+            line_point(L, i, cx, cy);
+            const uint8_t* sel = other + (size_t)(cy - k) * pitch + (cx - k);
+            unsigned acc = 0;
+            for (int v = 0; v < nbytes; v++)
+                acc = sad_row<ND>(sel + (size_t)v * pitch, kern + (size_t)v * pitch, lastmask,
+                                  nbytes, acc);
+            key = ((unsigned long long)acc << 32) | (unsigned)i;
+        }
+        key = wave_min_u64(key);                                      // :85 first min
+        best = key < best ? key : best;
+    }
+    if (lane == 0) {
+        int cx, cy;
+        line_point(L, (int)(best & 0xffffffffu), cx, cy);
+        const double dx = (double)(cx - x), dy = (double)(cy - y);
+        const int dn = (int)__builtin_sqrt(dx * dx + dy * dy);       // :89
+        disp_u8[p] = (uint8_t)dn;
+        if (disp_u16) disp_u16[p] = (uint16_t)dn;
+        if (valid_out) valid_out[p] = 1;
+    }
+}
+
+__global__ void disp_to_depth_kernel(const uint8_t* __restrict__ disp, int n, double num,
+                                     double pixel_size, double* __restrict__ depth) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double den = (double)disp[i] * pixel_size;   // multiply(disparity, pixelSize, .., 6)
+    depth[i] = den != 0.0 ? num / den : 0.0;          // camDistance * f / pixSizeDisp
+}
+
+}  // namespace
+
+hipError_t launch_ref_endpoints(Ctx& c, int W, int H, const sva_camera& cref,
+                                const sva_camera& coth, int k, double t_near, double t_far,
+                                int32_t* ends, uint8_t* valid) {
+    ScopedKernelTimer t(c, "ref_endpoints");
+    dim3 grid((W + 255) / 256, H);
+    hipLaunchKernelGGL(ref_endpoints_kernel, grid, dim3(256), 0, c.stream, W, H, cref, coth, k,
+                       t_near, t_far, (int4*)ends, valid);
+    return hipGetLastError();
+}
+
+#define SVA_REF_CASE(ND)                                                                       \
+    case ND:                                                                                   \
+        hipLaunchKernelGGL(ref_match_kernel<ND>, grid, dim3(256), 0, c.stream, ref, other, W, H, \
+                           pitch, mask, (const int4*)ends, valid_in, k, disp_u8, disp_u16,      \
+                           valid_out);                                                         \
+        break;
+
+hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, int W, int H,
+                            size_t pitch, const uint8_t* mask, const int32_t* ends,
+                            const uint8_t* valid_in, int k, uint8_t* disp_u8,
+                            uint16_t* disp_u16, uint8_t* valid_out) {
+    ScopedKernelTimer t(c, "ref_match");
+    const long long npx = (long long)(W - 2 * k) * (H - 2 * k);
+    if (npx <= 0) return hipSuccess;
+    dim3 grid((unsigned)((npx + 3) / 4));
+    switch ((k + 1) / 2) {  // ND = ceil(2k / 4)
+        SVA_REF_CASE(1) SVA_REF_CASE(2) SVA_REF_CASE(3) SVA_REF_CASE(4)
+        SVA_REF_CASE(5) SVA_REF_CASE(6) SVA_REF_CASE(7) SVA_REF_CASE(8)
+        SVA_REF_CASE(9) SVA_REF_CASE(10) SVA_REF_CASE(11) SVA_REF_CASE(12)
+        SVA_REF_CASE(13) SVA_REF_CASE(14) SVA_REF_CASE(15) SVA_REF_CASE(16)
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_disp_to_depth(Ctx& c, const uint8_t* disp, int n, double cam_distance,
+                                double f, double pixel_size, double* depth) {
+    ScopedKernelTimer t(c, "disp_to_depth");
+    const double num = cam_distance * f;
+    hipLaunchKernelGGL(disp_to_depth_kernel, dim3((n + 255) / 256), dim3(256), 0, c.stream, disp,
+                       n, num, pixel_size, depth);
+    return hipGetLastError();
+}
+
+}  // namespace sva

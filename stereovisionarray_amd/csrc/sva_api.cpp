@@ -1,0 +1,558 @@
+// sva_api.cpp -- the C-ABI of libsva.so (declared in include/sva.h).
+//
+// Host C++ only: argument validation, per-context device/stream/workspace
+// management, host<->device staging for the host-pointer entry points, the
+// hipEvent kernel timer and the multi-context batch driver.  Every compute
+// step is one of the HIP kernels in this directory; there is no CPU path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "sva_internal.h"
+
+using namespace sva;
+
+// ------------------------------------------------------------ internals --
+namespace sva {
+
+hipEvent_t KernelTimer::get_event() {
+    if (!pool.empty()) {
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+void KernelTimer::begin(hipStream_t s, const char*, hipEvent_t* start_out) {
+    hipEvent_t e = get_event();
+    if (e && hipEventRecord(e, s) == hipSuccess) *start_out = e;
+    else *start_out = nullptr;
+}
+
+void KernelTimer::end(hipStream_t s, const char* name, hipEvent_t start) {
+    hipEvent_t e = get_event();
+    if (!e) return;
+    if (hipEventRecord(e, s) != hipSuccess) { pool.push_back(e); return; }
+    pending.push_back(Pending{name, start, e});
+}
+
+hipError_t KernelTimer::resolve() {
+    hipError_t st = hipSuccess;
+    for (auto& p : pending) {
+        float ms = 0.f;
+        hipError_t e = hipEventSynchronize(p.stop);
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, p.start, p.stop);
+        if (e != hipSuccess) st = e;
+        auto& t = totals[p.name];
+        t.first += ms;
+        t.second += 1;
+        pool.push_back(p.start);
+        pool.push_back(p.stop);
+    }
+    pending.clear();
+    return st;
+}
+
+void KernelTimer::release_all() {
+    for (auto& p : pending) {
+        (void)hipEventDestroy(p.start);
+        (void)hipEventDestroy(p.stop);
+    }
+    pending.clear();
+    for (auto e : pool) (void)hipEventDestroy(e);
+    pool.clear();
+}
+
+hipError_t DevBuf::ensure(size_t n) {
+    if (n <= bytes && ptr) return hipSuccess;
+    if (ptr) {
+        (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    size_t want = std::max<size_t>(n, 256);
+    hipError_t e = hipMalloc(&ptr, want);
+    if (e != hipSuccess) {
+        ptr = nullptr;
+        return e;
+    }
+    bytes = want;
+    return hipSuccess;
+}
+
+void DevBuf::release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+}
+
+}  // namespace sva
+
+namespace {
+
+Ctx* as_ctx(void* p) { return static_cast<Ctx*>(p); }
+
+int fail(Ctx* c, int code, const std::string& msg) {
+    if (c) c->last_error = msg;
+    return code;
+}
+
+int hip_fail(Ctx* c, hipError_t e, const char* what) {
+    std::string m = std::string(what) + ": " + hipGetErrorString(e);
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation)
+        return fail(c, SVA_ERR_OUT_OF_MEMORY, m);
+    return fail(c, SVA_ERR_DEVICE, m);
+}
+
+#define SVA_HIP(c, expr, what)                           \
+    do {                                                 \
+        hipError_t _e = (expr);                          \
+        if (_e != hipSuccess) return hip_fail(c, _e, what); \
+    } while (0)
+
+#define SVA_CHECK_CTX(c)                                                       \
+    do {                                                                       \
+        if (!(c)) return SVA_ERR_INVALID_ARG;                                  \
+        if (hipSetDevice((c)->device) != hipSuccess)                           \
+            return fail(c, SVA_ERR_DEVICE, "hipSetDevice failed");             \
+    } while (0)
+
+int check_image(Ctx* c, const void* a, int W, int H, size_t pitch) {
+    if (!a) return fail(c, SVA_ERR_INVALID_ARG, "null image pointer");
+    if (W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "image size must be positive");
+    if (pitch < (size_t)W) return fail(c, SVA_ERR_INVALID_ARG, "pitch smaller than width");
+    if ((long long)W * H > (1ll << 31) - 1) return fail(c, SVA_ERR_INVALID_ARG, "image too large");
+    return SVA_OK;
+}
+
+int check_sgm(Ctx* c, const sva_sgm_params* p, int W) {
+    if (!p) return fail(c, SVA_ERR_INVALID_ARG, "null params");
+    if (p->D <= 0) return fail(c, SVA_ERR_INVALID_ARG, "D must be positive");
+    if (!paths_supported(p->D))
+        return fail(c, SVA_ERR_UNSUPPORTED, "GPU path built for D in {64,128,192,256}");
+    if (p->dir != 1 && p->dir != -1) return fail(c, SVA_ERR_INVALID_ARG, "dir must be +1 or -1");
+    if (p->dmin < 0) return fail(c, SVA_ERR_INVALID_ARG, "dmin must be >= 0");
+    if (p->P1 < 0 || p->P2 < 0 || p->P1 > 193 || p->P2 > 193)
+        return fail(c, SVA_ERR_INVALID_ARG, "penalties must satisfy 0 <= P1, P2 <= 193");
+    if (p->lr_check && p->lr_max_diff < 0)
+        return fail(c, SVA_ERR_INVALID_ARG, "lr_max_diff must be >= 0");
+    (void)W;
+    return SVA_OK;
+}
+
+// Mode S on device buffers: census -> cost -> 8 paths -> WTA (-> L/R check).
+int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int H, size_t pitch,
+                   const sva_sgm_params* p, uint16_t* disp, float* sub) {
+    const size_t np = (size_t)W * H, nv = np * (size_t)p->D;
+    SVA_HIP(c, c->census_l.ensure(np * 8), "census workspace");
+    SVA_HIP(c, c->census_r.ensure(np * 8), "census workspace");
+    SVA_HIP(c, c->cost.ensure(nv), "cost workspace");
+    SVA_HIP(c, c->paths.ensure(nv * 8), "path workspace");
+    uint64_t* cl = (uint64_t*)c->census_l.ptr;
+    uint64_t* cr = (uint64_t*)c->census_r.ptr;
+    uint8_t* C = (uint8_t*)c->cost.ptr;
+    uint8_t* L8 = (uint8_t*)c->paths.ptr;
+    SVA_HIP(c, launch_census(*c, left, W, H, pitch, cl), "census launch");
+    SVA_HIP(c, launch_census(*c, right, W, H, pitch, cr), "census launch");
+    SVA_HIP(c, launch_cost(*c, cl, cr, W, H, p->D, p->dmin, p->dir, C), "cost launch");
+    SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
+    SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, disp, sub), "wta launch");
+    if (p->lr_check) {
+        SVA_HIP(c, c->disp_r.ensure(np * 2), "lr workspace");
+        uint16_t* dr = (uint16_t*)c->disp_r.ptr;
+        // right image as reference: roles of the census maps swap, dir flips
+        SVA_HIP(c, launch_cost(*c, cr, cl, W, H, p->D, p->dmin, -p->dir, C), "cost launch");
+        SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
+        SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, dr, nullptr), "wta launch");
+        SVA_HIP(c, launch_lr_check(*c, disp, dr, W, H, p->dir, p->lr_max_diff, p->invalid),
+                "lr launch");
+    }
+    return SVA_OK;
+}
+
+int check_camera(Ctx* c, const sva_camera* cam) {
+    if (!cam) return fail(c, SVA_ERR_INVALID_ARG, "null camera");
+    return SVA_OK;
+}
+
+int run_ref_device(Ctx* c, const uint8_t* ref, const uint8_t* other, int W, int H, size_t pitch,
+                   const uint8_t* mask, const sva_camera* cref, const sva_camera* coth, int k,
+                   double t_near, double t_far, uint8_t* d8, uint16_t* d16, uint8_t* valid) {
+    const size_t np = (size_t)W * H;
+    SVA_HIP(c, c->census_l.ensure(np * 16), "endpoint workspace");
+    SVA_HIP(c, c->census_r.ensure(np), "endpoint workspace");
+    int32_t* ends = (int32_t*)c->census_l.ptr;
+    uint8_t* ok = (uint8_t*)c->census_r.ptr;
+    SVA_HIP(c, launch_ref_endpoints(*c, W, H, *cref, *coth, k, t_near, t_far, ends, ok),
+            "endpoint launch");
+    SVA_HIP(c, launch_ref_match(*c, ref, other, W, H, pitch, mask, ends, ok, k, d8, d16, valid),
+            "match launch");
+    return SVA_OK;
+}
+
+int check_ref_args(Ctx* c, int W, int H, int k, double t_near, double t_far) {
+    if (k < 1 || k > 32) return fail(c, SVA_ERR_UNSUPPORTED, "kernel half-size k must be 1..32");
+    if (2 * k >= W || 2 * k >= H) return fail(c, SVA_ERR_INVALID_ARG, "image smaller than window");
+    if (!(t_near > 0.0) || !(t_far > 0.0))
+        return fail(c, SVA_ERR_INVALID_ARG, "ray parameters must be positive");
+    if (W > 4095 || H > 4095)
+        return fail(c, SVA_ERR_UNSUPPORTED, "Mode R supports W, H < 4096");
+    return SVA_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ ABI --
+extern "C" {
+
+void sva_sgm_params_default(sva_sgm_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->D = 128;
+    p->dmin = 0;
+    p->dir = -1;
+    p->P1 = 10;
+    p->P2 = 120;
+    p->subpixel = 0;
+    p->lr_check = 0;
+    p->lr_max_diff = 1;
+    p->invalid = 0xffff;
+}
+
+int sva_abi_version(void) { return SVA_ABI_VERSION; }
+
+int sva_device_count(int* count) {
+    if (!count) return SVA_ERR_INVALID_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return SVA_OK;
+}
+
+const char* sva_status_string(int s) {
+    switch (s) {
+        case SVA_OK: return "ok";
+        case SVA_ERR_INVALID_ARG: return "invalid argument";
+        case SVA_ERR_UNSUPPORTED: return "unsupported configuration";
+        case SVA_ERR_DEVICE: return "device error";
+        case SVA_ERR_OUT_OF_MEMORY: return "out of device memory";
+        case SVA_ERR_NO_DEVICE: return "no usable HIP device";
+        default: return "unknown status";
+    }
+}
+
+int sva_create(int device, void** out) {
+    if (!out) return SVA_ERR_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return SVA_ERR_NO_DEVICE;
+    if (device < 0 || device >= n) return SVA_ERR_INVALID_ARG;
+    if (hipSetDevice(device) != hipSuccess) return SVA_ERR_DEVICE;
+    Ctx* c = new (std::nothrow) Ctx();
+    if (!c) return SVA_ERR_OUT_OF_MEMORY;
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return SVA_ERR_DEVICE;
+    }
+    c->stream = c->own_stream;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->cu_count = prop.multiProcessorCount;
+    *out = c;
+    return SVA_OK;
+}
+
+int sva_destroy(void* ctx) {
+    Ctx* c = as_ctx(ctx);
+    if (!c) return SVA_ERR_INVALID_ARG;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (DevBuf* b : {&c->census_l, &c->census_r, &c->cost, &c->paths, &c->scratch_u16,
+                      &c->disp_r, &c->in_a, &c->in_b, &c->in_mask, &c->out_a, &c->out_b,
+                      &c->out_c})
+        b->release();
+    c->timer.release_all();
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return SVA_OK;
+}
+
+int sva_set_stream(void* ctx, void* stream) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    c->stream = stream ? (hipStream_t)stream : c->own_stream;
+    return SVA_OK;
+}
+
+int sva_synchronize(void* ctx) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    SVA_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    return SVA_OK;
+}
+
+const char* sva_last_error(void* ctx) {
+    Ctx* c = as_ctx(ctx);
+    return c ? c->last_error.c_str() : "null context";
+}
+
+int sva_reserve(void* ctx, int W, int H, int D) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    if (W <= 0 || H <= 0 || D <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad reserve size");
+    const size_t np = (size_t)W * H, nv = np * (size_t)D;
+    SVA_HIP(c, c->census_l.ensure(np * 16), "reserve");
+    SVA_HIP(c, c->census_r.ensure(np * 8), "reserve");
+    SVA_HIP(c, c->cost.ensure(nv), "reserve");
+    SVA_HIP(c, c->paths.ensure(nv * 8), "reserve");
+    return SVA_OK;
+}
+
+int sva_set_timing(void* ctx, int enable) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    c->timer.enabled = enable != 0;
+    return SVA_OK;
+}
+
+int sva_reset_timing(void* ctx) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    hipError_t e = c->timer.resolve();
+    c->timer.totals.clear();
+    if (e != hipSuccess) return hip_fail(c, e, "timer resolve");
+    return SVA_OK;
+}
+
+int sva_kernel_time(void* ctx, const char* name, double* total_ms, int64_t* count) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    if (!name || !total_ms || !count) return fail(c, SVA_ERR_INVALID_ARG, "null argument");
+    hipError_t e = c->timer.resolve();
+    if (e != hipSuccess) return hip_fail(c, e, "timer resolve");
+    auto it = c->timer.totals.find(name);
+    *total_ms = it == c->timer.totals.end() ? 0.0 : it->second.first;
+    *count = it == c->timer.totals.end() ? 0 : it->second.second;
+    return SVA_OK;
+}
+
+// ---------------------------------------------------------------- Mode S --
+int sva_disparity_sgm_d(void* ctx, const uint8_t* left, const uint8_t* right, int W, int H,
+                        size_t pitch, const sva_sgm_params* p, uint16_t* disp, float* sub) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_image(c, left, W, H, pitch)) || (s = check_image(c, right, W, H, pitch)) ||
+        (s = check_sgm(c, p, W)))
+        return s;
+    if (!disp) return fail(c, SVA_ERR_INVALID_ARG, "null disparity output");
+    return run_sgm_device(c, left, right, W, H, pitch, p, disp, p->subpixel ? sub : nullptr);
+}
+
+int sva_disparity_sgm(void* ctx, const uint8_t* left, const uint8_t* right, int W, int H,
+                      size_t pitch, const sva_sgm_params* p, uint16_t* disp, float* sub) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_image(c, left, W, H, pitch)) || (s = check_image(c, right, W, H, pitch)) ||
+        (s = check_sgm(c, p, W)))
+        return s;
+    if (!disp) return fail(c, SVA_ERR_INVALID_ARG, "null disparity output");
+    const bool want_sub = p->subpixel && sub;
+    const size_t np = (size_t)W * H;
+    SVA_HIP(c, c->in_a.ensure(np), "staging");
+    SVA_HIP(c, c->in_b.ensure(np), "staging");
+    SVA_HIP(c, c->out_a.ensure(np * 2), "staging");
+    if (want_sub) SVA_HIP(c, c->out_b.ensure(np * 4), "staging");
+    SVA_HIP(c, hipMemcpy2DAsync(c->in_a.ptr, W, left, pitch, W, H, hipMemcpyHostToDevice, c->stream),
+            "upload");
+    SVA_HIP(c, hipMemcpy2DAsync(c->in_b.ptr, W, right, pitch, W, H, hipMemcpyHostToDevice, c->stream),
+            "upload");
+    if ((s = run_sgm_device(c, (uint8_t*)c->in_a.ptr, (uint8_t*)c->in_b.ptr, W, H, W, p,
+                            (uint16_t*)c->out_a.ptr, want_sub ? (float*)c->out_b.ptr : nullptr)))
+        return s;
+    SVA_HIP(c, hipMemcpyAsync(disp, c->out_a.ptr, np * 2, hipMemcpyDeviceToHost, c->stream),
+            "download");
+    if (want_sub)
+        SVA_HIP(c, hipMemcpyAsync(sub, c->out_b.ptr, np * 4, hipMemcpyDeviceToHost, c->stream),
+                "download");
+    SVA_HIP(c, hipStreamSynchronize(c->stream), "sync");
+    return SVA_OK;
+}
+
+int sva_census_d(void* ctx, const uint8_t* img, int W, int H, size_t pitch, uint64_t* census) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_image(c, img, W, H, pitch))) return s;
+    if (!census) return fail(c, SVA_ERR_INVALID_ARG, "null census output");
+    SVA_HIP(c, launch_census(*c, img, W, H, pitch, census), "census launch");
+    return SVA_OK;
+}
+
+int sva_cost_d(void* ctx, const uint64_t* cl, const uint64_t* cr, int W, int H,
+               const sva_sgm_params* p, uint8_t* C) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_sgm(c, p, W))) return s;
+    if (!cl || !cr || !C || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
+    SVA_HIP(c, launch_cost(*c, cl, cr, W, H, p->D, p->dmin, p->dir, C), "cost launch");
+    return SVA_OK;
+}
+
+int sva_paths_d(void* ctx, const uint8_t* C, int W, int H, const sva_sgm_params* p, uint8_t* L8) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_sgm(c, p, W))) return s;
+    if (!C || !L8 || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
+    SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
+    return SVA_OK;
+}
+
+int sva_aggregate_d(void* ctx, const uint8_t* C, int W, int H, const sva_sgm_params* p,
+                    uint16_t* S) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_sgm(c, p, W))) return s;
+    if (!C || !S || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
+    const size_t nv = (size_t)W * H * (size_t)p->D;
+    SVA_HIP(c, c->paths.ensure(nv * 8), "path workspace");
+    uint8_t* L8 = (uint8_t*)c->paths.ptr;
+    SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
+    SVA_HIP(c, launch_sum(*c, L8, W, H, p->D, S), "sum launch");
+    return SVA_OK;
+}
+
+int sva_wta_d(void* ctx, const uint16_t* S, int W, int H, const sva_sgm_params* p, uint16_t* disp,
+              float* sub) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_sgm(c, p, W))) return s;
+    if (!S || !disp || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
+    SVA_HIP(c, launch_wta_from_sum(*c, S, W, H, p->D, p->dmin, disp, p->subpixel ? sub : nullptr),
+            "wta launch");
+    return SVA_OK;
+}
+
+// ---------------------------------------------------------------- Mode R --
+int sva_ref_endpoints_d(void* ctx, int W, int H, const sva_camera* cref, const sva_camera* coth,
+                        int k, double t_near, double t_far, int32_t* ends, uint8_t* valid) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_camera(c, cref)) || (s = check_camera(c, coth)) ||
+        (s = check_ref_args(c, W, H, k, t_near, t_far)))
+        return s;
+    if (!ends || !valid) return fail(c, SVA_ERR_INVALID_ARG, "null output");
+    SVA_HIP(c, launch_ref_endpoints(*c, W, H, *cref, *coth, k, t_near, t_far, ends, valid),
+            "endpoint launch");
+    return SVA_OK;
+}
+
+int sva_disparity_ref_d(void* ctx, const uint8_t* ref, const uint8_t* other, int W, int H,
+                        size_t pitch, const uint8_t* mask, const sva_camera* cref,
+                        const sva_camera* coth, int k, double t_near, double t_far, uint8_t* d8,
+                        uint16_t* d16, uint8_t* valid) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_image(c, ref, W, H, pitch)) || (s = check_image(c, other, W, H, pitch)) ||
+        (s = check_camera(c, cref)) || (s = check_camera(c, coth)) ||
+        (s = check_ref_args(c, W, H, k, t_near, t_far)))
+        return s;
+    if (!d8) return fail(c, SVA_ERR_INVALID_ARG, "null disparity output");
+    return run_ref_device(c, ref, other, W, H, pitch, mask, cref, coth, k, t_near, t_far, d8, d16,
+                          valid);
+}
+
+int sva_disparity_ref(void* ctx, const uint8_t* ref, const uint8_t* other, int W, int H,
+                      size_t pitch, const uint8_t* mask, const sva_camera* cref,
+                      const sva_camera* coth, int k, double t_near, double t_far, uint8_t* d8,
+                      uint16_t* d16, uint8_t* valid) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_image(c, ref, W, H, pitch)) || (s = check_image(c, other, W, H, pitch)) ||
+        (s = check_camera(c, cref)) || (s = check_camera(c, coth)) ||
+        (s = check_ref_args(c, W, H, k, t_near, t_far)))
+        return s;
+    if (!d8) return fail(c, SVA_ERR_INVALID_ARG, "null disparity output");
+    const size_t np = (size_t)W * H;
+    SVA_HIP(c, c->in_a.ensure(np), "staging");
+    SVA_HIP(c, c->in_b.ensure(np), "staging");
+    SVA_HIP(c, c->out_a.ensure(np), "staging");
+    if (mask) SVA_HIP(c, c->in_mask.ensure(np), "staging");
+    if (d16) SVA_HIP(c, c->out_b.ensure(np * 2), "staging");
+    if (valid) SVA_HIP(c, c->out_c.ensure(np), "staging");
+    hipStream_t st = c->stream;
+    SVA_HIP(c, hipMemcpy2DAsync(c->in_a.ptr, W, ref, pitch, W, H, hipMemcpyHostToDevice, st), "upload");
+    SVA_HIP(c, hipMemcpy2DAsync(c->in_b.ptr, W, other, pitch, W, H, hipMemcpyHostToDevice, st), "upload");
+    if (mask) SVA_HIP(c, hipMemcpyAsync(c->in_mask.ptr, mask, np, hipMemcpyHostToDevice, st), "upload");
+    // untouched pixels keep the caller's values (CameraStereoVision.cpp:46,55)
+    SVA_HIP(c, hipMemcpyAsync(c->out_a.ptr, d8, np, hipMemcpyHostToDevice, st), "upload");
+    if (d16) SVA_HIP(c, hipMemcpyAsync(c->out_b.ptr, d16, np * 2, hipMemcpyHostToDevice, st), "upload");
+    if (valid) SVA_HIP(c, hipMemcpyAsync(c->out_c.ptr, valid, np, hipMemcpyHostToDevice, st), "upload");
+    if ((s = run_ref_device(c, (uint8_t*)c->in_a.ptr, (uint8_t*)c->in_b.ptr, W, H, W,
+                            mask ? (uint8_t*)c->in_mask.ptr : nullptr, cref, coth, k, t_near,
+                            t_far, (uint8_t*)c->out_a.ptr, d16 ? (uint16_t*)c->out_b.ptr : nullptr,
+                            valid ? (uint8_t*)c->out_c.ptr : nullptr)))
+        return s;
+    SVA_HIP(c, hipMemcpyAsync(d8, c->out_a.ptr, np, hipMemcpyDeviceToHost, st), "download");
+    if (d16) SVA_HIP(c, hipMemcpyAsync(d16, c->out_b.ptr, np * 2, hipMemcpyDeviceToHost, st), "download");
+    if (valid) SVA_HIP(c, hipMemcpyAsync(valid, c->out_c.ptr, np, hipMemcpyDeviceToHost, st), "download");
+    SVA_HIP(c, hipStreamSynchronize(st), "sync");
+    return SVA_OK;
+}
+
+int sva_disparity_to_depth_d(void* ctx, const uint8_t* disp, int n, double cam_distance,
+                             double f, double pixel_size, double* depth) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    if (!disp || !depth || n < 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
+    if (n == 0) return SVA_OK;
+    SVA_HIP(c, launch_disp_to_depth(*c, disp, n, cam_distance, f, pixel_size, depth), "depth launch");
+    return SVA_OK;
+}
+
+// ---------------------------------------------------------------- batch --
+int sva_batch_sgm(void** ctxs, int n_ctx, const sva_pair_job* jobs, int n_jobs,
+                  const sva_sgm_params* p) {
+    if (!ctxs || n_ctx <= 0 || (n_jobs > 0 && !jobs) || n_jobs < 0 || !p)
+        return SVA_ERR_INVALID_ARG;
+    for (int i = 0; i < n_ctx; i++)
+        if (!ctxs[i]) return SVA_ERR_INVALID_ARG;
+    std::vector<int> status(n_ctx, SVA_OK);
+    std::vector<std::thread> th;
+    for (int i = 0; i < n_ctx; i++) {
+        th.emplace_back([&, i]() {
+            for (int j = i; j < n_jobs; j += n_ctx) {  // pair j -> context j mod N
+                const sva_pair_job& J = jobs[j];
+                int s = sva_disparity_sgm(ctxs[i], J.left, J.right, J.width, J.height, J.pitch, p,
+                                          J.disp, J.subpix);
+                if (s != SVA_OK) {
+                    status[i] = s;
+                    return;
+                }
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int s : status)
+        if (s != SVA_OK) return s;
+    return SVA_OK;
+}
+
+}  // extern "C"

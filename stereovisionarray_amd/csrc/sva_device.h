@@ -1,0 +1,65 @@
+// sva_device.h -- CDNA4 (gfx950) device helpers shared by the kernels:
+// packed-u16 SIMD types and wave64 DPP cross-lane primitives.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace sva {
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ unsigned as_u32(u16x2 v) { return __builtin_bit_cast(unsigned, v); }
+__device__ __forceinline__ u16x2 as_v2(unsigned v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ u16x2 splat2(unsigned v) {
+    return (u16x2){(unsigned short)v, (unsigned short)v};
+}
+__device__ __forceinline__ u16x2 vmin2(u16x2 a, u16x2 b) { return __builtin_elementwise_min(a, b); }
+
+// DPP control words (GFX9 encoding).
+enum : int {
+    DPP_QUAD_1032 = 0xb1,       // quad_perm [1,0,3,2]
+    DPP_QUAD_2301 = 0x4e,       // quad_perm [2,3,0,1]
+    DPP_ROW_SHL1 = 0x101,       // lane i <- lane i+1 within a 16-lane row
+    DPP_ROW_SHR1 = 0x111,       // lane i <- lane i-1 within a 16-lane row
+    DPP_ROW_MIRROR = 0x140,     // lane i <- lane 15-i
+    DPP_ROW_HALF_MIRROR = 0x141 // lane i <- lane 7-i within each half row
+};
+
+// Lane i of each 16-lane row receives lane i-1's value; lane 0 receives `edge`.
+__device__ __forceinline__ unsigned row_shr1(unsigned v, unsigned edge) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)edge, (int)v, DPP_ROW_SHR1, 0xf, 0xf, false);
+}
+// Lane i of each 16-lane row receives lane i+1's value; lane 15 receives `edge`.
+__device__ __forceinline__ unsigned row_shl1(unsigned v, unsigned edge) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)edge, (int)v, DPP_ROW_SHL1, 0xf, 0xf, false);
+}
+
+// Minimum over the 16 lanes of a DPP row, result broadcast to all 16 lanes.
+__device__ __forceinline__ unsigned row_min_u32(unsigned v) {
+    unsigned x;
+    x = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_QUAD_1032, 0xf, 0xf, false);
+    v = v < x ? v : x;
+    x = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_QUAD_2301, 0xf, 0xf, false);
+    v = v < x ? v : x;
+    x = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_HALF_MIRROR, 0xf, 0xf, false);
+    v = v < x ? v : x;
+    x = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_MIRROR, 0xf, 0xf, false);
+    v = v < x ? v : x;
+    return v;
+}
+
+// Unpack 4 u8 (one dword) into two u16x2 pairs: (b0,b1) and (b2,b3).
+__device__ __forceinline__ void unpack4(unsigned w, unsigned& p01, unsigned& p23) {
+    // v_perm_b32 selector: byte k of result = sel byte; 0x0c = zero.
+    p01 = __builtin_amdgcn_perm(0u, w, 0x0c010c00u);
+    p23 = __builtin_amdgcn_perm(0u, w, 0x0c030c02u);
+}
+// Pack two u16x2 pairs (values < 256) into one dword of 4 u8.
+__device__ __forceinline__ unsigned pack4(unsigned p01, unsigned p23) {
+    // result bytes: [p01.b0, p01.b2, p23.b0, p23.b2]; src0 = p23 (bytes 4..7), src1 = p01 (0..3)
+    return __builtin_amdgcn_perm(p23, p01, 0x06040200u);
+}
+
+}  // namespace sva

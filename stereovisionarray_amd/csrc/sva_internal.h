@@ -1,0 +1,107 @@
+// sva_internal.h -- context, workspace and kernel-launcher declarations shared
+// by the C-ABI (sva_api.cpp) and the HIP kernel translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/sva.h"
+
+namespace sva {
+
+// Host-side status carrier: every launcher returns hipError_t, the API maps it.
+struct Status {
+    int code = SVA_OK;
+    std::string msg;
+};
+
+// Per-kernel hipEvent timing on the context stream.  Events are only recorded
+// while timing is enabled; resolution happens lazily in kernel_time().
+struct KernelTimer {
+    bool enabled = false;
+    struct Pending {
+        std::string name;
+        hipEvent_t start, stop;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> pool;
+    std::map<std::string, std::pair<double, int64_t>> totals;  // ms, count
+
+    hipEvent_t get_event();
+    void begin(hipStream_t s, const char* name, hipEvent_t* start_out);
+    void end(hipStream_t s, const char* name, hipEvent_t start);
+    hipError_t resolve();  // fold pending into totals (synchronises on each stop event)
+    void release_all();
+};
+
+// Device workspace grown on demand (never shrinks within a context).
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n);
+    void release();
+};
+
+struct Ctx {
+    int device = -1;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+    KernelTimer timer;
+    // Mode S workspace
+    DevBuf census_l, census_r, cost, paths, scratch_u16, disp_r;
+    // host-pointer staging
+    DevBuf in_a, in_b, in_mask, out_a, out_b, out_c;
+    int cu_count = 256;
+};
+
+// RAII helper: records timing events around one launch when enabled.
+struct ScopedKernelTimer {
+    Ctx& c;
+    const char* name;
+    hipEvent_t start = nullptr;
+    ScopedKernelTimer(Ctx& ctx, const char* n) : c(ctx), name(n) {
+        if (c.timer.enabled) c.timer.begin(c.stream, name, &start);
+    }
+    ~ScopedKernelTimer() {
+        if (c.timer.enabled && start) c.timer.end(c.stream, name, start);
+    }
+};
+
+// ------------------------------------------------------------- launchers --
+// All launchers enqueue on ctx.stream and return the launch status.
+
+// census.hip
+hipError_t launch_census(Ctx& c, const uint8_t* img, int W, int H, size_t pitch, uint64_t* out);
+// cost.hip
+hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,
+                       int dmin, int dir, uint8_t* C);
+// sgm_paths.hip -- all 8 directions in one launch; L8 = [8][H][W][D] u8.
+hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
+                        uint8_t* L8);
+bool paths_supported(int D);
+// wta.hip
+hipError_t launch_sum(Ctx& c, const uint8_t* L8, int W, int H, int D, uint16_t* S);
+hipError_t launch_wta_from_paths(Ctx& c, const uint8_t* L8, int W, int H, int D, int dmin,
+                                 uint16_t* disp, float* sub);
+hipError_t launch_wta_from_sum(Ctx& c, const uint16_t* S, int W, int H, int D, int dmin,
+                               uint16_t* disp, float* sub);
+hipError_t launch_lr_check(Ctx& c, uint16_t* disp_l, const uint16_t* disp_r, int W, int H,
+                           int dir, int max_diff, uint16_t invalid);
+// refpath.hip
+hipError_t launch_ref_endpoints(Ctx& c, int W, int H, const sva_camera& cref,
+                                const sva_camera& coth, int k, double t_near, double t_far,
+                                int32_t* ends, uint8_t* valid);
+hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, int W, int H,
+                            size_t pitch, const uint8_t* mask, const int32_t* ends,
+                            const uint8_t* valid_in, int k, uint8_t* disp_u8,
+                            uint16_t* disp_u16, uint8_t* valid_out);
+// depth.hip
+hipError_t launch_disp_to_depth(Ctx& c, const uint8_t* disp, int n, double cam_distance,
+                                double f, double pixel_size, double* depth);
+
+}  // namespace sva

@@ -1,0 +1,208 @@
+// wta.hip -- path sum, winner-take-all and sub-pixel (DESIGN.md §2.4,
+// SURVEY.md §8a row A13), plus the left/right check (§2.5).
+//
+// Same lane layout as sgm_paths.hip: one 16-lane DPP row per pixel, lane k
+// holds disparities [k*DPL, k*DPL+DPL).  S = sum of the 8 u8 path volumes is
+// formed in packed u16 (no carry: S <= 8*255 < 2^16), the first minimum is a
+// u32 min over keys (S << 16 | d) -- the smaller d wins ties, mirroring
+// std::min_element at CameraStereoVision.cpp:85 -- reduced across the row by
+// DPP.  S(d*-1), S(d*+1) for the parabola are fetched with a DPP OR-reduce.
+#include "sva_device.h"
+#include "sva_internal.h"
+
+namespace sva {
+namespace {
+
+constexpr int BLOCK = 256;
+constexpr int PIX_PER_BLOCK = BLOCK / 16;
+
+__device__ __forceinline__ unsigned row_or_u32(unsigned v) {
+    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_QUAD_1032, 0xf, 0xf, false);
+    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_QUAD_2301, 0xf, 0xf, false);
+    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_HALF_MIRROR, 0xf, 0xf, false);
+    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_MIRROR, 0xf, 0xf, false);
+    return v;
+}
+
+template <int NW>
+__device__ __forceinline__ void load_nw(const uint8_t* p, unsigned (&w)[NW]) {
+    if constexpr (NW == 1) {
+        w[0] = *(const unsigned*)p;
+    } else if constexpr (NW == 2) {
+        uint2 v = *(const uint2*)p;
+        w[0] = v.x; w[1] = v.y;
+    } else if constexpr (NW == 3) {
+        const unsigned* q = (const unsigned*)p;
+        w[0] = q[0]; w[1] = q[1]; w[2] = q[2];
+    } else {
+        uint4 v = *(const uint4*)p;
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    }
+}
+
+// S pairs for this lane from the 8 direction volumes.
+template <int DPL>
+__device__ __forceinline__ void sum_paths(const uint8_t* p, size_t vol, unsigned (&S)[DPL / 2]) {
+    constexpr int NW = DPL / 4, NP = DPL / 2;
+#pragma unroll
+    for (int j = 0; j < NP; j++) S[j] = 0u;
+    unsigned w[8][NW];
+#pragma unroll
+    for (int r = 0; r < 8; r++) load_nw<NW>(p + (size_t)r * vol, w[r]);
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+#pragma unroll
+        for (int q = 0; q < NW; q++) {
+            unsigned a, b;
+            unpack4(w[r][q], a, b);
+            S[2 * q] += a;      // packed add, no carry across halves
+            S[2 * q + 1] += b;
+        }
+}
+
+template <int DPL>
+__device__ __forceinline__ void wta_finish(const unsigned (&S)[DPL / 2], int k, int D, int dmin,
+                                           size_t pix, uint16_t* disp, float* sub) {
+    constexpr int NP = DPL / 2;
+    const int d0 = k * DPL;
+    unsigned best = 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+        unsigned lo = ((S[j] & 0xffffu) << 16) | (unsigned)(d0 + 2 * j);
+        unsigned hi = (S[j] & 0xffff0000u) | (unsigned)(d0 + 2 * j + 1);
+        best = best < lo ? best : lo;
+        best = best < hi ? best : hi;
+    }
+    best = row_min_u32(best);
+    const int ds = (int)(best & 0xffffu);
+    float v = (float)(dmin + ds);
+    if (sub) {
+        unsigned vm = 0, vp = 0;
+#pragma unroll
+        for (int j = 0; j < NP; j++) {
+            const int da = d0 + 2 * j;
+            const unsigned lo = S[j] & 0xffffu, hi = S[j] >> 16;
+            vm = (da == ds - 1) ? lo : vm;
+            vm = (da + 1 == ds - 1) ? hi : vm;
+            vp = (da == ds + 1) ? lo : vp;
+            vp = (da + 1 == ds + 1) ? hi : vp;
+        }
+        vm = row_or_u32(vm);
+        vp = row_or_u32(vp);
+        if (ds > 0 && ds < D - 1) {
+            const int a = (int)vm, b = (int)(best >> 16), c = (int)vp;
+            const int den = a - 2 * b + c;
+            if (den > 0) v = v + (float)(a - c) / (float)(2 * den);
+        }
+    }
+    if (k == 0) {
+        disp[pix] = (uint16_t)(dmin + ds);
+        if (sub) sub[pix] = v;
+    }
+}
+
+template <int DPL>
+__global__ __launch_bounds__(BLOCK) void wta_paths_kernel(const uint8_t* __restrict__ L8,
+                                                          size_t vol, int npix, int D, int dmin,
+                                                          uint16_t* __restrict__ disp,
+                                                          float* __restrict__ sub) {
+    const size_t pix = (size_t)blockIdx.x * PIX_PER_BLOCK + (threadIdx.x >> 4);
+    const int k = threadIdx.x & 15;
+    if (pix >= (size_t)npix) return;
+    unsigned S[DPL / 2];
+    sum_paths<DPL>(L8 + pix * D + k * DPL, vol, S);
+    wta_finish<DPL>(S, k, D, dmin, pix, disp, sub);
+}
+
+template <int DPL>
+__global__ __launch_bounds__(BLOCK) void sum_paths_kernel(const uint8_t* __restrict__ L8,
+                                                          size_t vol, int npix, int D,
+                                                          uint16_t* __restrict__ Sout) {
+    const size_t pix = (size_t)blockIdx.x * PIX_PER_BLOCK + (threadIdx.x >> 4);
+    const int k = threadIdx.x & 15;
+    if (pix >= (size_t)npix) return;
+    unsigned S[DPL / 2];
+    sum_paths<DPL>(L8 + pix * D + k * DPL, vol, S);
+    unsigned* o = (unsigned*)(Sout + pix * D + k * DPL);
+#pragma unroll
+    for (int j = 0; j < DPL / 2; j++) o[j] = S[j];
+}
+
+template <int DPL>
+__global__ __launch_bounds__(BLOCK) void wta_sum_kernel(const uint16_t* __restrict__ Sin,
+                                                        int npix, int D, int dmin,
+                                                        uint16_t* __restrict__ disp,
+                                                        float* __restrict__ sub) {
+    const size_t pix = (size_t)blockIdx.x * PIX_PER_BLOCK + (threadIdx.x >> 4);
+    const int k = threadIdx.x & 15;
+    if (pix >= (size_t)npix) return;
+    unsigned S[DPL / 2];
+    const unsigned* s = (const unsigned*)(Sin + pix * D + k * DPL);
+#pragma unroll
+    for (int j = 0; j < DPL / 2; j++) S[j] = s[j];
+    wta_finish<DPL>(S, k, D, dmin, pix, disp, sub);
+}
+
+__global__ void lr_check_kernel(uint16_t* __restrict__ dl, const uint16_t* __restrict__ dr, int W,
+                                int H, int dir, int max_diff, uint16_t invalid) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= W) return;
+    uint16_t* p = dl + (size_t)y * W + x;
+    const int d = *p;
+    if (d == invalid) return;
+    const int xr = x + dir * d;
+    if (xr < 0 || xr >= W) { *p = invalid; return; }
+    const int r = dr[(size_t)y * W + xr];
+    const int diff = d > r ? d - r : r - d;
+    if (r == invalid || diff > max_diff) *p = invalid;
+}
+
+}  // namespace
+
+#define SVA_DISPATCH_D(D, KERNEL, GRID, ...)                                                     \
+    switch (D) {                                                                                 \
+        case 64: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(BLOCK), 0, c.stream, __VA_ARGS__); break;   \
+        case 128: hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(BLOCK), 0, c.stream, __VA_ARGS__); break;  \
+        case 192: hipLaunchKernelGGL(KERNEL<12>, GRID, dim3(BLOCK), 0, c.stream, __VA_ARGS__); break; \
+        case 256: hipLaunchKernelGGL(KERNEL<16>, GRID, dim3(BLOCK), 0, c.stream, __VA_ARGS__); break; \
+        default: return hipErrorInvalidValue;                                                    \
+    }
+
+hipError_t launch_wta_from_paths(Ctx& c, const uint8_t* L8, int W, int H, int D, int dmin,
+                                 uint16_t* disp, float* sub) {
+    ScopedKernelTimer t(c, "wta");
+    const int npix = W * H;
+    const size_t vol = (size_t)npix * D;
+    dim3 grid((npix + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK);
+    SVA_DISPATCH_D(D, wta_paths_kernel, grid, L8, vol, npix, D, dmin, disp, sub);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum(Ctx& c, const uint8_t* L8, int W, int H, int D, uint16_t* S) {
+    ScopedKernelTimer t(c, "path_sum");
+    const int npix = W * H;
+    const size_t vol = (size_t)npix * D;
+    dim3 grid((npix + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK);
+    SVA_DISPATCH_D(D, sum_paths_kernel, grid, L8, vol, npix, D, S);
+    return hipGetLastError();
+}
+
+hipError_t launch_wta_from_sum(Ctx& c, const uint16_t* S, int W, int H, int D, int dmin,
+                               uint16_t* disp, float* sub) {
+    ScopedKernelTimer t(c, "wta_sum");
+    const int npix = W * H;
+    dim3 grid((npix + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK);
+    SVA_DISPATCH_D(D, wta_sum_kernel, grid, S, npix, D, dmin, disp, sub);
+    return hipGetLastError();
+}
+
+hipError_t launch_lr_check(Ctx& c, uint16_t* disp_l, const uint16_t* disp_r, int W, int H,
+                           int dir, int max_diff, uint16_t invalid) {
+    ScopedKernelTimer t(c, "lr_check");
+    dim3 grid((W + 255) / 256, H);
+    hipLaunchKernelGGL(lr_check_kernel, grid, dim3(256), 0, c.stream, disp_l, disp_r, W, H, dir,
+                       max_diff, invalid);
+    return hipGetLastError();
+}
+
+}  // namespace sva

@@ -1,0 +1,245 @@
+"""Known-answer tests that pin the CPU oracle (no GPU needed).
+
+The reference ships no tests or golden vectors and cannot be built here
+(OpenCV absent), so the oracle is "parity unpinned" with respect to the
+reference binary.  These KATs are hand-derived from the reference source
+(functions.cpp:253-321, Camera.cpp:15-34, CameraStereoVision.cpp:85-89) and
+from the Mode S spec; each expected value below was traced by
+hand, not produced by the code under test.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from stereovisionarray_amd import synth
+
+
+# -------------------------------------------------------------- Bresenham --
+# Hand traces of plotLineLow/plotLineHigh (functions.cpp:253-297) as selected
+# by bresenham(point2, point1) (:299-321) called with (pixel1, pixel2).
+BRESENHAM_KAT = [
+    (((0, 0), (3, 1)), [(0, 0), (1, 0), (2, 1), (3, 1)]),
+    (((3, 1), (0, 0)), [(0, 0), (1, 0), (2, 1), (3, 1)]),          # emitted from lower x
+    (((5, 5), (4, 9)), [(5, 5), (5, 6), (5, 7), (4, 8), (4, 9)]),  # High, xi = -1
+    (((4, 9), (5, 5)), [(5, 5), (5, 6), (5, 7), (4, 8), (4, 9)]),  # emitted from lower y
+    (((0, 0), (2, 2)), [(0, 0), (1, 1), (2, 2)]),                  # |dx| == |dy| -> High
+    (((4, 4), (4, 4)), [(4, 4)]),                                  # single point
+    (((0, 2), (4, 0)), [(0, 2), (1, 2), (2, 1), (3, 1), (4, 0)]),  # Low, yi = -1
+    (((10, 10), (20, 13)), [(10, 10), (11, 10), (12, 11), (13, 11), (14, 11), (15, 11),
+                            (16, 12), (17, 12), (18, 12), (19, 13), (20, 13)]),
+]
+
+
+@pytest.mark.parametrize("args,expected", BRESENHAM_KAT)
+def test_bresenham_kat(oracle, args, expected):
+    assert oracle.bresenham(*args) == expected
+
+
+def test_bresenham_closed_form(oracle):
+    """The GPU kernel enumerates candidate i in O(1):
+    Low: (x0+i, y0 + yi*floor((2|dy|i + dx - 1)/(2dx))), High transposed.
+    Check that formula against the oracle's iterative trace on many lines."""
+    rng = np.random.RandomState(0)
+    for _ in range(3000):
+        p1 = tuple(int(v) for v in rng.randint(-40, 40, 2))
+        p2 = tuple(int(v) for v in rng.randint(-40, 40, 2))
+        pts = oracle.bresenham(p1, p2)
+        (ax, ay), (bx, by) = p1, p2
+        if abs(ay - by) < abs(ax - bx):
+            x0, y0, x1, y1 = (ax, ay, bx, by) if bx > ax else (bx, by, ax, ay)
+            dx, dy = x1 - x0, abs(y1 - y0)
+            s = -1 if y1 < y0 else 1
+            exp = [(x0 + i, y0 + s * ((2 * dy * i + dx - 1) // (2 * dx))) for i in range(dx + 1)]
+        else:
+            x0, y0, x1, y1 = (ax, ay, bx, by) if by > ay else (bx, by, ax, ay)
+            dy, dx = y1 - y0, abs(x1 - x0)
+            s = -1 if x1 < x0 else 1
+            if dy == 0:
+                exp = [(x0, y0)]
+            else:
+                exp = [(x0 + s * ((2 * dx * i + dy - 1) // (2 * dy)), y0 + i) for i in range(dy + 1)]
+        assert pts == exp, (p1, p2)
+
+
+# ----------------------------------------------------------------- Camera --
+def test_project_truncates_toward_zero(oracle):
+    # f = 0.05, pixel 0.036/640: mult = 0.05/(0.25+0.75)/5.625e-5 = 888.88..
+    cam = oracle.OCamera.make(0.05, (0.0, 0.0, -0.75), 0.036 / 640)
+    assert oracle.project(cam, (0.01, -0.02, 0.25)) == (8, -17)   # 8.88 -> 8, -17.77 -> -17
+
+
+def test_inv_project_3_4_12(oracle):
+    cam = oracle.OCamera.make(12.0, (0.0, 0.0, 0.0), 1.0)
+    assert oracle.inv_project(cam, 3, 4) == (3 / 13, 4 / 13, 12 / 13)
+
+
+def test_endpoints_second_restatement(oracle):
+    """Independent Python restatement of CameraStereoVision.cpp:28,60-71 and
+    Camera.cpp:15-33 (IEEE doubles, same operand order) vs the C oracle."""
+    W, H, k = 640, 480, 20
+    ps = 0.036 / W
+    grid = synth.reference_array(ps)
+    for (ir, io) in [(12, 11), (12, 7), (12, 18), (12, 6)]:
+        f, pr, _ = grid[ir]
+        _, po, _ = grid[io]
+        cref = oracle.OCamera.make(*grid[ir])
+        coth = oracle.OCamera.make(*grid[io])
+        hx, hy = W // 2, H // 2
+        for y in range(k, H - k, 37):
+            for x in range(k, W - k, 29):
+                v = ((x - hx) * ps, (y - hy) * ps, f)
+                n = math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
+                e = (v[0] / n, v[1] / n, v[2] / n)
+                out = []
+                for t in (0.5, 1.0):
+                    P = [pr[i] + e[i] * t for i in range(3)]
+                    mult = f / (P[2] - po[2]) / ps
+                    out.append((int((P[0] - po[0]) * mult) + hx, int((P[1] - po[1]) * mult) + hy))
+                ok = all(not (p[0] < k or p[1] < k or p[0] > W - k or p[1] > H - k) for p in out)
+                got = oracle.ref_endpoints(cref, coth, W, H, k, 0.5, 1.0, x, y)
+                assert got == (ok, out[0], out[1]), (ir, io, x, y)
+
+
+def test_reference_geometry_candidate_counts(oracle):
+    """with the reference rig, pair 12/11 at 640 px wide has
+    45-49 candidates per pixel."""
+    W, H, k = 640, 480, 20
+    grid = synth.reference_array(0.036 / W)
+    cref, coth = oracle.OCamera.make(*grid[12]), oracle.OCamera.make(*grid[11])
+    counts = []
+    for y in range(k, H - k, 23):
+        for x in range(k, W - k, 19):
+            ok, a, b = oracle.ref_endpoints(cref, coth, W, H, k, 0.5, 1.0, x, y)
+            if ok:
+                counts.append(len(oracle.bresenham(a, b)))
+    assert min(counts) >= 45 and max(counts) <= 49
+
+
+# -------------------------------------------------------------------- SAD --
+def test_sad_kat(oracle):
+    a = np.array([[0, 255], [10, 20]], np.uint8)
+    b = np.array([[255, 0], [20, 10]], np.uint8)
+    assert oracle.lib.svo_sad(a.ctypes.data, 2, b.ctypes.data, 2, 2, 2) == 530
+
+
+def test_ref_pair_constant_images_pick_first_candidate(oracle):
+    """All SADs 0 -> std::min_element returns index 0, the first emitted point
+    (lowest x for a Low line) -> disparity = |first - (x,y)| truncated."""
+    W, H, k = 160, 120, 6
+    grid = synth.reference_array(0.036 / W)
+    cref, coth = oracle.OCamera.make(*grid[12]), oracle.OCamera.make(*grid[11])
+    img = np.full((H, W), 90, np.uint8)
+    d8, d16, valid, _ = oracle.ref_pair(img, img, cref, coth, k=k)
+    for y, x in [(40, 40), (60, 80), (100, 120)]:
+        ok, a, b = oracle.ref_endpoints(cref, coth, W, H, k, 0.5, 1.0, x, y)
+        assert valid[y, x] == ok
+        if ok:
+            first = oracle.bresenham(a, b)[0]
+            assert d16[y, x] == int(math.sqrt((first[0] - x) ** 2 + (first[1] - y) ** 2))
+
+
+def test_depth_kat(oracle):
+    d = np.array([0, 1, 2, 255], np.uint8)
+    out = oracle.disp_to_depth(d, 0.05, 0.05, 0.036 / 640)
+    num = 0.05 * 0.05
+    assert out[0] == 0.0
+    assert out[1] == num / (1.0 * (0.036 / 640))
+    assert out[3] == num / (255.0 * (0.036 / 640))
+
+
+# ----------------------------------------------------------------- Census --
+def _census_window_image(center=100, fill=150):
+    img = np.full((7, 9), fill, np.uint8)
+    img[3, 4] = center
+    return img
+
+
+def test_census_kat(oracle):
+    img = _census_window_image()
+    assert int(oracle.census(img)[3, 4]) == 0                 # nothing darker
+    img[0, 0] = 50                                            # first window element
+    assert int(oracle.census(img)[3, 4]) == 1 << 61
+    img = _census_window_image()
+    img[6, 8] = 50                                            # last window element
+    assert int(oracle.census(img)[3, 4]) == 1
+    img = _census_window_image()
+    img[3, 3] = 50                                            # just left of centre: e = 3*8+3 = 30
+    assert int(oracle.census(img)[3, 4]) == 1 << (61 - 30)
+    img = _census_window_image(center=100, fill=100)          # equal is not '<'
+    assert int(oracle.census(img)[3, 4]) == 0
+    c = oracle.census(_census_window_image())
+    assert (c[np.arange(7) != 3].sum() == 0) and c[3, :4].sum() == 0  # borders are 0
+
+
+def test_cost_kat(oracle):
+    cl = np.array([[0b1011, 0, 0b1111]], np.uint64)
+    cr = np.array([[0b0001, 0b0110, 0]], np.uint64)
+    C = oracle.cost(cl, cr, D=2, dmin=0, dir=1)
+    # x=0: d0 pop(1011^0001)=2, d1 pop(1011^0110)=3; x=1: pop(0^0110)=2, pop(0^0)=0;
+    # x=2: d0 pop(1111^0)=4, d1 -> column 3 outside -> 62
+    assert C[0].tolist() == [[2, 3], [2, 0], [4, 62]]
+    C = oracle.cost(cl, cr, D=2, dmin=1, dir=-1)
+    # x=0: col -1,-2 outside; x=1: d0 col 0 -> pop(0^1)=1, d1 col -1 -> 62; x=2: col 1 -> pop(1111^0110)=2, col 0 -> pop(1111^0001)=3
+    assert C[0].tolist() == [[62, 62], [1, 62], [2, 3]]
+
+
+# -------------------------------------------------------------------- SGM --
+C1D = np.array([[[0, 5, 9], [3, 3, 3], [9, 0, 9], [1, 1, 1]]], np.uint8)  # H=1, W=4, D=3
+
+
+def test_path_1d_hand_expanded(oracle):
+    """P1=2, P2=6 recurrence expanded by hand."""
+    L0 = oracle.path(C1D, 0, P1=2, P2=6)   # left -> right
+    assert L0[0].tolist() == [[0, 5, 9], [3, 5, 9], [9, 2, 13], [3, 1, 3]]
+    L1 = oracle.path(C1D, 1, P1=2, P2=6)   # right -> left
+    assert L1[0].tolist() == [[2, 5, 11], [5, 3, 5], [9, 0, 9], [1, 1, 1]]
+    for r in range(2, 8):                  # H = 1: every pixel starts a path
+        assert np.array_equal(oracle.path(C1D, r, P1=2, P2=6), C1D)
+    S = oracle.aggregate(C1D, P1=2, P2=6)
+    assert np.array_equal(S, L0.astype(np.uint16) + L1 + 6 * C1D.astype(np.uint16))
+
+
+def test_path_bounds(oracle):
+    rng = np.random.RandomState(1)
+    C = rng.randint(0, 63, size=(9, 11, 16)).astype(np.uint8)
+    for r in range(8):
+        L = oracle.path(C, r).astype(int)
+        assert (L >= C).all() and (L <= C.astype(int) + 120).all()
+        assert (L.min(axis=2) <= C.astype(int).max(axis=2)).all()
+
+
+def test_wta_kat(oracle):
+    S = np.array([[[5, 3, 3, 7]]], np.uint16)
+    d, s = oracle.wta(S, dmin=10)
+    assert d[0, 0] == 11                 # first of the tied minima
+    assert s[0, 0] == np.float32(11.5)   # a=5 b=3 c=3: (5-3)/(2*2)
+    S = np.array([[[1, 3, 3, 7]]], np.uint16)
+    d, s = oracle.wta(S, dmin=0)
+    assert d[0, 0] == 0 and s[0, 0] == 0.0   # edge: no parabola
+
+
+def test_sgm_shifted_texture(oracle):
+    W, H, D, d0 = 160, 48, 32, 9
+    L = synth.texture(H, W, 4)
+    R = np.zeros_like(L)
+    R[:, : W - d0] = L[:, d0:]
+    d, _ = oracle.sgm(L, R, D, 0, -1, subpixel=False)
+    assert (d[6:-6, d0 + 24: W - 24] == d0).all()
+
+
+def test_sgm_threads_identical(oracle):
+    L, R, _ = synth.stereo_pair(40, 90, 64, 0, -1, seed=2)
+    a, sa = oracle.sgm(L, R, 64, threads=1)
+    b, sb = oracle.sgm(L, R, 64, threads=4)
+    assert np.array_equal(a, b) and np.array_equal(sa, sb)
+
+
+def test_lr_check_kat(oracle):
+    dl = np.array([[0, 2, 2, 1]], np.uint16)
+    dr = np.array([[0, 3, 2, 9]], np.uint16)
+    out = oracle.lr_check(dl, dr, dir=-1, max_diff=0, invalid=0xFFFF)
+    # x=0: xr=0 dr=0 ok; x=1: xr=-1 outside; x=2: xr=0, dr=0 vs 2 -> reject; x=3: xr=2 dr=2 vs 1 -> reject
+    assert out[0].tolist() == [0, 0xFFFF, 0xFFFF, 0xFFFF]
+    out = oracle.lr_check(dl, dr, dir=-1, max_diff=2, invalid=0xFFFF)
+    assert out[0].tolist() == [0, 0xFFFF, 2, 1]

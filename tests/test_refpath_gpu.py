@@ -1,0 +1,131 @@
+"""Mode R parity: the reference's own path (CameraStereoVision.cpp:44-95) on
+the GPU vs the CPU restatement (oracle/refpath_oracle.c), bit-exact.
+
+Parity of the restatement against the reference binary is unpinned (the
+reference needs OpenCV, absent here); tests/test_oracle_kat.py pins the
+restatement by hand-derived known answers instead.
+"""
+import numpy as np
+import pytest
+import torch
+
+from stereovisionarray_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def cams_for(sva, oracle, W, i_ref, i_oth):
+    ps = 0.036 / W  # pixelSize = sensor_size / width (CameraStereoVision.cpp:30)
+    grid = synth.reference_array(ps)
+    return (sva.Camera.make(*grid[i_ref]), sva.Camera.make(*grid[i_oth]),
+            oracle.OCamera.make(*grid[i_ref]), oracle.OCamera.make(*grid[i_oth]))
+
+
+# pairs from getCameraPairs (functions.cpp:148-197): MID_LEFT, MID_TOP and the
+# diagonal TO_CENTER_SMALL members, so Low and High Bresenham lines and both
+# step signs are exercised.
+PAIRS = [(12, 11), (12, 13), (12, 7), (12, 17), (12, 6), (12, 8), (12, 16), (12, 18)]
+
+
+@pytest.mark.parametrize("W,H", [(160, 120), (640, 480), (1920, 1080), (3840, 2160), (321, 243)])
+@pytest.mark.parametrize("pair", [(12, 11), (12, 7), (12, 18)])
+def test_endpoints_bit_exact(ctx, sva, oracle, torch_dev, W, H, pair):
+    """f64 ray geometry: every pixel's (pixel1, pixel2) and the bounds check,
+    including the ~19% of 1080p pixels whose row truncates off by one."""
+    cr, co, ocr, oco = cams_for(sva, oracle, W, *pair)
+    k = 20
+    ends = torch.zeros((H, W, 4), dtype=torch.int32, device=torch_dev)
+    valid = torch.zeros((H, W), dtype=torch.uint8, device=torch_dev)
+    ctx.ref_endpoints_d(W, H, cr, co, k, 0.5, 1.0, ends.data_ptr(), valid.data_ptr())
+    ctx.synchronize()
+    e = ends.cpu().numpy()
+    v = valid.cpu().numpy()
+    rng = np.random.RandomState(W + pair[1])
+    ys = np.concatenate([rng.randint(k, H - k, 400), [k, H - k - 1, H // 2]])
+    xs = np.concatenate([rng.randint(k, W - k, 400), [k, W - k - 1, W // 2]])
+    for y, x in zip(ys, xs):
+        ok, a, b = oracle.ref_endpoints(ocr, oco, W, H, k, 0.5, 1.0, int(x), int(y))
+        assert tuple(e[y, x]) == (a[0], a[1], b[0], b[1]), (x, y)
+        assert bool(v[y, x]) == ok, (x, y)
+
+
+@pytest.mark.parametrize("pair", PAIRS)
+def test_ref_path_pairs(ctx, sva, oracle, pair):
+    W, H, k = 160, 120, 12
+    cr, co, ocr, oco = cams_for(sva, oracle, W, *pair)
+    img_ref = synth.texture(H, W, pair[1])
+    img_oth = synth.texture(H, W, 100 + pair[1])
+    # embed a shifted copy so the minimum is meaningful
+    img_oth[:, 12:] = img_ref[:, :-12]
+    d8, d16, valid = ctx.disparity_ref(img_ref, img_oth, cr, co, k=k)
+    o8, o16, ovalid, n = oracle.ref_pair(img_ref, img_oth, ocr, oco, k=k)
+    assert n > 0
+    assert np.array_equal(valid, ovalid)
+    assert np.array_equal(d8, o8)
+    assert np.array_equal(d16, o16)
+
+
+@pytest.mark.parametrize("k", [1, 3, 8, 20, 21, 32])
+def test_ref_path_window_sizes(ctx, sva, oracle, k):
+    """Windows 2k x 2k incl. odd k (2k % 4 == 2: partial last dword)."""
+    W, H = 200, 150
+    cr, co, ocr, oco = cams_for(sva, oracle, W, 12, 11)
+    a = synth.texture(H, W, k)
+    b = np.roll(a, 10, axis=1)
+    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k)
+    o8, o16, ovalid, _ = oracle.ref_pair(a, b, ocr, oco, k=k)
+    assert np.array_equal(valid, ovalid) and np.array_equal(d16, o16)
+
+
+def test_ref_path_mask_and_overwrite(ctx, sva, oracle):
+    """mask == 0 pixels are skipped (:53) and keep the caller's values; a
+    second pair overwrites only the pixels it keeps (:55)."""
+    W, H, k = 160, 120, 10
+    cr, co, ocr, oco = cams_for(sva, oracle, W, 12, 11)
+    _, co2, _, oco2 = cams_for(sva, oracle, W, 12, 7)
+    a = synth.texture(H, W, 1)
+    b = np.roll(a, 8, axis=1)
+    c = np.roll(a, 8, axis=0)
+    mask = np.zeros((H, W), np.uint8)
+    mask[20:90, 30:140] = 255
+    g8 = np.full((H, W), 77, np.uint8)
+    g16 = np.full((H, W), 777, np.uint16)
+    gv = np.zeros((H, W), np.uint8)
+    ctx.disparity_ref(a, b, cr, co, k=k, mask=mask, disp_u8=g8, disp_u16=g16, valid=gv)
+    ctx.disparity_ref(a, c, cr, co2, k=k, mask=mask, disp_u8=g8, disp_u16=g16, valid=gv)
+    o8 = np.full((H, W), 77, np.uint8)
+    o16 = np.full((H, W), 777, np.uint16)
+    ov = np.zeros((H, W), np.uint8)
+    oracle.ref_pair(a, b, ocr, oco, k=k, mask=mask, disp_u8=o8, disp_u16=o16, valid=ov)
+    oracle.ref_pair(a, c, ocr, oco2, k=k, mask=mask, disp_u8=o8, disp_u16=o16, valid=ov)
+    assert np.array_equal(g8, o8) and np.array_equal(g16, o16) and np.array_equal(gv, ov)
+    assert (g8[mask == 0] == 77).all()
+
+
+def test_ref_path_wraps_mod_256(ctx, sva, oracle):
+    """1080p-class geometry: disparities above 255 wrap in the u8 map (:89)
+    while the u16 map keeps them."""
+    W, H, k = 1920, 64, 20
+    ps = 0.036 / W
+    grid = synth.reference_array(ps)
+    # cameras 12 and 10 (JUMP_CROSS, functions.cpp:191) are 0.1 m apart
+    cr, co = sva.Camera.make(*grid[12]), sva.Camera.make(*grid[10])
+    ocr, oco = oracle.OCamera.make(*grid[12]), oracle.OCamera.make(*grid[10])
+    a = synth.texture(H, W, 5)
+    b = np.roll(a, 300, axis=1)
+    mask = np.zeros((H, W), np.uint8)
+    mask[30:34, 700:1200] = 1
+    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k, mask=mask)
+    o8, o16, ov, _ = oracle.ref_pair(a, b, ocr, oco, k=k, mask=mask)
+    assert np.array_equal(valid, ov) and np.array_equal(d16, o16) and np.array_equal(d8, o8)
+    assert (d16[valid == 1] > 255).any()
+
+
+def test_depth(ctx, oracle, torch_dev):
+    disp = np.arange(256, dtype=np.uint8).repeat(3)
+    cam_distance, f, ps = 0.05, 0.05, 0.036 / 640
+    d = torch.from_numpy(disp).to(torch_dev)
+    out = torch.zeros(disp.size, dtype=torch.float64, device=torch_dev)
+    ctx.disparity_to_depth_d(d.data_ptr(), disp.size, cam_distance, f, ps, out.data_ptr())
+    ctx.synchronize()
+    assert np.array_equal(out.cpu().numpy(), oracle.disp_to_depth(disp, cam_distance, f, ps))

@@ -1,0 +1,27 @@
+#!/bin/bash
+# One GPU-box session: each GPU step under its own time limit; stop at the
+# first step that faults / aborts / times out (exit codes other than 0 and 1).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+run() {
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"; tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case "$step" in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    pytest) run pytest_gpu 1200 python -m pytest tests -q -m "gpu and not slow" -x ;;
+    pytest_all) run pytest_gpu_all 1500 python -m pytest tests -q -m gpu ;;
+    pytest_slow) run pytest_gpu_slow 900 python -m pytest tests -q -m "gpu and slow" ;;
+    bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    bench4k) run bench4k 600 python bench.py --steps 5 --warmup 2 --workload 4k_d256 --no-cpu-baseline ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
