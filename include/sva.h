@@ -146,6 +146,8 @@ int sva_ref_endpoints_d(void* ctx, int width, int height, const sva_camera* ref_
 /* Disparity -> depth, CameraStereoVision.cpp:47,98-100 (f64; 0 where disp 0). */
 int sva_disparity_to_depth_d(void* ctx, const uint8_t* disp, int n, double cam_distance,
                              double f, double pixel_size, double* depth);
+int sva_disparity_to_depth(void* ctx, const uint8_t* disp, int n, double cam_distance,
+                           double f, double pixel_size, double* depth);
 
 /* -------------------------------------------------- multi-pair batch --- */
 /* Independent pairs round-robin over the given contexts (one per device),

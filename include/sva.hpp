@@ -1,0 +1,336 @@
+// sva.hpp -- C++ host mirror of the reference's interface for the stereo hot
+// path, layered on the C-ABI in sva.h.  Header-only; no OpenCV, no torch.
+//
+// It keeps the reference's names, argument meaning and error behaviour so a
+// call site in CameraStereoVision.cpp reads the same:
+//   Camera               include/Camera.h:6-21, src/Camera.cpp:6-34
+//   pairType             include/functions.h:8-19
+//   getCameraPairs       src/functions.cpp:148-213 (incl. the :205 quirk, opt-out)
+//   getGroups            src/functions.cpp:107-116
+//   bresenham            src/functions.cpp:253-321
+//   getAbsDiff           src/functions.cpp:215-218 (on raw 8-bit views)
+//   computeDisparity     NEW: replaces the inline hot loop
+//                        src/CameraStereoVision.cpp:44-95 with one GPU call
+//   disparityToDepth     src/CameraStereoVision.cpp:47,98-100
+// Host-side helpers (Camera math, bresenham, pair tables) run on the CPU as in
+// the reference -- they are per-call scalars, not the hot path.  Everything
+// per-pixel runs on the GPU through sva.h.  Errors are reported as
+// sva::Error exceptions on the C++ side (the reference throws cv::Exception on
+// bad input); nothing throws across the C-ABI itself.
+#pragma once
+
+#include <array>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "sva.h"
+
+namespace sva {
+
+struct Point2i {
+    int x = 0, y = 0;
+    Point2i() = default;
+    Point2i(int x_, int y_) : x(x_), y(y_) {}
+    Point2i operator+(const Point2i& o) const { return {x + o.x, y + o.y}; }
+    Point2i operator-(const Point2i& o) const { return {x - o.x, y - o.y}; }
+    bool operator==(const Point2i& o) const { return x == o.x && y == o.y; }
+};
+
+struct Point3d {
+    double x = 0, y = 0, z = 0;
+    Point3d() = default;
+    Point3d(double x_, double y_, double z_) : x(x_), y(y_), z(z_) {}
+    Point3d operator+(const Point3d& o) const { return {x + o.x, y + o.y, z + o.z}; }
+    Point3d operator-(const Point3d& o) const { return {x - o.x, y - o.y, z - o.z}; }
+    Point3d operator*(double s) const { return {x * s, y * s, z * s}; }
+    Point3d operator/(double s) const { return {x / s, y / s, z / s}; }
+};
+
+inline double norm(const Point3d& p) { return std::sqrt(p.x * p.x + p.y * p.y + p.z * p.z); }
+inline double norm(const Point2i& p) {
+    return std::sqrt((double)p.x * p.x + (double)p.y * p.y);
+}
+
+struct Error : std::runtime_error {
+    int status;
+    Error(int s, const std::string& m) : std::runtime_error(m), status(s) {}
+};
+
+// class Camera -- include/Camera.h:6-21 (public fields, same constructor).
+class Camera {
+public:
+    Camera(double focal_length, Point3d position, double pixel_size_)
+        : pos3D(position), f(focal_length), pixel_size(pixel_size_) {}
+
+    Point3d pos3D;
+    double f;
+    double pixel_size;
+
+    // Camera::project (src/Camera.cpp:15-21): truncation toward zero.
+    Point2i project(Point3d P) const {
+        double mult = f / (P.z - pos3D.z) / pixel_size;
+        return {int((P.x - pos3D.x) * mult), int((P.y - pos3D.y) * mult)};
+    }
+    // Camera::inv_project (src/Camera.cpp:25-33).
+    Point3d inv_project(Point2i px) const {
+        Point3d v{px.x * pixel_size, px.y * pixel_size, f};
+        return v / norm(v);
+    }
+    sva_camera abi() const {
+        sva_camera c;
+        c.f = f;
+        c.pos[0] = pos3D.x;
+        c.pos[1] = pos3D.y;
+        c.pos[2] = pos3D.z;
+        c.pixel_size = pixel_size;
+        return c;
+    }
+};
+
+// include/functions.h:8-19
+enum pairType {
+    ORTHOGONAL,
+    DIAGONAL,
+    TO_CENTER,
+    LINE_HORIZONTAL,
+    LINE_VERTICAL,
+    CROSS,
+    JUMP_CROSS,
+    TO_CENTER_SMALL,
+    MID_LEFT,
+    MID_TOP
+};
+
+// getCameraPairs(cameras, pairType) -- src/functions.cpp:148-197.
+inline std::vector<std::array<int, 2>> getCameraPairs(const std::vector<Camera>& cameras,
+                                                      const pairType pair) {
+    std::vector<std::array<int, 2>> pairs;
+    const int n = (int)cameras.size();
+    switch (pair) {
+        case TO_CENTER:
+            for (int i = 0; i < n; i++)
+                if (i != 12) pairs.push_back({12, i});
+            break;
+        case TO_CENTER_SMALL:
+            for (int o : {6, 7, 8, 11, 13, 16, 17, 18}) pairs.push_back({12, o});
+            break;
+        case MID_LEFT: pairs.push_back({12, 11}); break;
+        case MID_TOP: pairs.push_back({12, 7}); break;
+        case LINE_HORIZONTAL:
+            for (int i = 10; i < 15; i++)
+                if (i != 12) pairs.push_back({12, i});
+            break;
+        case LINE_VERTICAL:
+            for (int i = 2; i < 25; i += 5)
+                if (i != 12) pairs.push_back({12, i});
+            break;
+        case CROSS:
+            for (int o : {11, 13, 7, 17}) pairs.push_back({12, o});
+            break;
+        case JUMP_CROSS:
+            for (int o : {10, 14, 2, 24}) pairs.push_back({12, o});
+            break;
+        default: break;  // ORTHOGONAL, DIAGONAL: empty in the reference too
+    }
+    return pairs;
+}
+
+// getCameraPairs(cameras, CROSS, cameraNum) -- src/functions.cpp:199-213.
+// reference_quirks = true reproduces the reference exactly: the second entry
+// is {cameraNum, +5} (the literal camera 5, :205) and the upward neighbour is
+// only added for cameraNum - 5 > 0 (:202).  false gives the evident intent.
+inline std::vector<std::array<int, 2>> getCameraPairs(const std::vector<Camera>& cameras,
+                                                      const pairType pair, int cameraNum,
+                                                      bool reference_quirks = true) {
+    (void)cameras;
+    std::vector<std::array<int, 2>> pairs;
+    if (pair != CROSS) return pairs;
+    if (reference_quirks ? (cameraNum - 5 > 0) : (cameraNum - 5 >= 0))
+        pairs.push_back({cameraNum, cameraNum - 5});
+    if (cameraNum + 5 < 25) pairs.push_back({cameraNum, reference_quirks ? 5 : cameraNum + 5});
+    if (cameraNum % 5 > 0) pairs.push_back({cameraNum, cameraNum - 1});
+    if (cameraNum % 5 < 4) pairs.push_back({cameraNum, cameraNum + 1});
+    return pairs;
+}
+
+// getGroups -- src/functions.cpp:107-116 ("CHESS": CROSS groups of 0,2,..,24).
+inline std::vector<std::vector<std::array<int, 2>>> getGroups(std::vector<Camera>& cameras,
+                                                              const std::string& groupType,
+                                                              bool reference_quirks = true) {
+    std::vector<std::vector<std::array<int, 2>>> groups;
+    if (groupType == "CHESS")
+        for (int i = 0; i < 25; i += 2)
+            groups.push_back(getCameraPairs(cameras, CROSS, i, reference_quirks));
+    return groups;
+}
+
+// bresenham(point2, point1) -- src/functions.cpp:253-321 (first parameter is
+// the caller's pixel1).  Emits from the lower x (|dy| < |dx|) or lower y.
+inline std::vector<Point2i> bresenham(Point2i point2, Point2i point1) {
+    std::vector<Point2i> pts;
+    auto low = [&](int x0, int y0, int x1, int y1) {
+        int dx = x1 - x0, dy = y1 - y0, yi = 1;
+        if (dy < 0) { yi = -1; dy = -dy; }
+        int D = 2 * dy - dx, y = y0;
+        for (int x = x0; x <= x1; x++) {
+            pts.push_back({x, y});
+            if (D > 0) { y += yi; D -= 2 * dx; }
+            D += 2 * dy;
+        }
+    };
+    auto high = [&](int x0, int y0, int x1, int y1) {
+        int dx = x1 - x0, dy = y1 - y0, xi = 1;
+        if (dx < 0) { xi = -1; dx = -dx; }
+        int D = 2 * dx - dy, x = x0;
+        for (int y = y0; y <= y1; y++) {
+            pts.push_back({x, y});
+            if (D > 0) { x += xi; D -= 2 * dy; }
+            D += 2 * dx;
+        }
+    };
+    if (std::abs(point2.y - point1.y) < std::abs(point2.x - point1.x)) {
+        if (point1.x > point2.x) low(point2.x, point2.y, point1.x, point1.y);
+        else low(point1.x, point1.y, point2.x, point2.y);
+    } else {
+        if (point1.y > point2.y) high(point2.x, point2.y, point1.x, point1.y);
+        else high(point1.x, point1.y, point2.x, point2.y);
+    }
+    return pts;
+}
+
+// Non-owning 8-bit image view (the part of cv::Mat the path uses).
+struct ImageView {
+    const uint8_t* data = nullptr;
+    int width = 0, height = 0;
+    size_t pitch = 0;  // bytes per row
+    ImageView() = default;
+    ImageView(const uint8_t* d, int w, int h, size_t p = 0)
+        : data(d), width(w), height(h), pitch(p ? p : (size_t)w) {}
+    ImageView roi(int x, int y, int w, int h) const {
+        if (x < 0 || y < 0 || x + w > width || y + h > height)
+            throw Error(SVA_ERR_INVALID_ARG, "roi outside image");  // cv::Mat throws here too
+        return ImageView(data + (size_t)y * pitch + x, w, h, pitch);
+    }
+};
+
+// getAbsDiff -- src/functions.cpp:215-218: sum |m1 - m2| as double.
+// Compatibility helper for call sites outside the hot path (e.g. one-off
+// checks); computeDisparity never calls it -- its SADs run on the GPU.
+inline double getAbsDiff(const ImageView& m1, const ImageView& m2) {
+    if (m1.width != m2.width || m1.height != m2.height)
+        throw Error(SVA_ERR_INVALID_ARG, "getAbsDiff: size mismatch");
+    int64_t s = 0;
+    for (int v = 0; v < m1.height; v++)
+        for (int u = 0; u < m1.width; u++) {
+            int d = (int)m1.data[v * m1.pitch + u] - (int)m2.data[v * m2.pitch + u];
+            s += d < 0 ? -d : d;
+        }
+    return (double)s;
+}
+
+// RAII owner of one sva context (one device, one stream).
+class Engine {
+public:
+    explicit Engine(int device = 0) {
+        int s = sva_create(device, &ctx_);
+        if (s != SVA_OK) throw Error(s, std::string("sva_create: ") + sva_status_string(s));
+    }
+    ~Engine() {
+        if (ctx_) sva_destroy(ctx_);
+    }
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+    void* handle() const { return ctx_; }
+    void check(int s) const {
+        if (s != SVA_OK) throw Error(s, sva_last_error(ctx_));
+    }
+
+private:
+    void* ctx_ = nullptr;
+};
+
+// Result of computeDisparity: the reference's CV_8UC1 map (values wrap mod
+// 256, CameraStereoVision.cpp:89), the unwrapped map and a validity mask
+// (the reference leaves skipped pixels uninitialised, :46).
+struct DisparityMaps {
+    int width = 0, height = 0;
+    std::vector<uint8_t> disp_u8;
+    std::vector<uint16_t> disp_u16;
+    std::vector<uint8_t> valid;
+};
+
+// Replaces CameraStereoVision.cpp:44-95 (pairs loop incl. last-pair-wins).
+// mask may be empty (width 0): every pixel selected.
+inline DisparityMaps computeDisparity(Engine& eng, const std::vector<ImageView>& images,
+                                      const std::vector<Camera>& cameras,
+                                      const std::vector<std::array<int, 2>>& pairs,
+                                      const ImageView& mask, int kernelSize,
+                                      double t_near = 0.5, double t_far = 1.0) {
+    if (pairs.empty()) throw Error(SVA_ERR_INVALID_ARG, "no camera pairs");
+    const ImageView& first = images.at(pairs[0][0]);
+    DisparityMaps out;
+    out.width = first.width;
+    out.height = first.height;
+    const size_t n = (size_t)first.width * first.height;
+    out.disp_u8.assign(n, 0);
+    out.disp_u16.assign(n, 0);
+    out.valid.assign(n, 0);
+    std::vector<uint8_t> mask_dense;
+    const uint8_t* mptr = nullptr;
+    if (mask.data && mask.width) {
+        if (mask.width != first.width || mask.height != first.height)
+            throw Error(SVA_ERR_INVALID_ARG, "mask size mismatch");
+        mask_dense.resize(n);
+        for (int y = 0; y < mask.height; y++)
+            for (int x = 0; x < mask.width; x++)
+                mask_dense[(size_t)y * mask.width + x] = mask.data[(size_t)y * mask.pitch + x];
+        mptr = mask_dense.data();
+    }
+    for (const auto& pr : pairs) {
+        const ImageView& a = images.at(pr[0]);
+        const ImageView& b = images.at(pr[1]);
+        if (a.width != b.width || a.height != b.height || a.pitch != b.pitch)
+            throw Error(SVA_ERR_INVALID_ARG, "pair images differ in size");
+        const sva_camera ca = cameras.at(pr[0]).abi(), cb = cameras.at(pr[1]).abi();
+        eng.check(sva_disparity_ref(eng.handle(), a.data, b.data, a.width, a.height, a.pitch, mptr,
+                                    &ca, &cb, kernelSize, t_near, t_far, out.disp_u8.data(),
+                                    out.disp_u16.data(), out.valid.data()));
+    }
+    return out;
+}
+
+// Mode S matcher on one rectified pair (north_star SGM).
+inline std::vector<uint16_t> computeDisparitySGM(Engine& eng, const ImageView& left,
+                                                 const ImageView& right,
+                                                 const sva_sgm_params& p,
+                                                 std::vector<float>* subpix = nullptr) {
+    if (left.width != right.width || left.height != right.height || left.pitch != right.pitch)
+        throw Error(SVA_ERR_INVALID_ARG, "pair images differ in size");
+    std::vector<uint16_t> disp((size_t)left.width * left.height);
+    float* sp = nullptr;
+    if (subpix && p.subpixel) {
+        subpix->resize(disp.size());
+        sp = subpix->data();
+    }
+    eng.check(sva_disparity_sgm(eng.handle(), left.data, right.data, left.width, left.height,
+                                left.pitch, &p, disp.data(), sp));
+    return disp;
+}
+
+// CameraStereoVision.cpp:47,98-100 on the GPU (per-pixel f64; reference:
+// multiply(disparity, pixelSize, .., CV_64F) then camDistance * f /
+// pixSizeDisp, 0 where the divisor is 0).
+inline std::vector<double> disparityToDepth(Engine& eng, const std::vector<uint8_t>& disparity,
+                                            const Camera& c0, const Camera& c1) {
+    const double camDistance = norm(c0.pos3D - c1.pos3D);
+    std::vector<double> depth(disparity.size());
+    eng.check(sva_disparity_to_depth(eng.handle(), disparity.data(), (int)disparity.size(),
+                                     camDistance, c0.f, c0.pixel_size, depth.data()));
+    return depth;
+}
+
+}  // namespace sva

@@ -13,7 +13,6 @@ from __future__ import annotations
 
 import ctypes as ct
 import os
-from dataclasses import dataclass
 
 import numpy as np
 
@@ -35,6 +34,7 @@ EXPORTED = [
     "sva_kernel_time", "sva_disparity_sgm", "sva_disparity_sgm_d", "sva_census_d",
     "sva_cost_d", "sva_paths_d", "sva_aggregate_d", "sva_wta_d", "sva_disparity_ref",
     "sva_disparity_ref_d", "sva_ref_endpoints_d", "sva_disparity_to_depth_d",
+    "sva_disparity_to_depth",
     "sva_batch_sgm",
 ]
 
@@ -76,7 +76,23 @@ class SvaError(RuntimeError):
         self.status = status
 
 
+def _preload_single_hip_runtime() -> None:
+    """Keep ONE HIP runtime per process.  PyTorch-ROCm wheels bundle their own
+    libamdhip64 (same SONAME as /opt/rocm's).  If libsva.so were loaded first it
+    would bind /opt/rocm's copy and a later `import torch` would map a second
+    runtime whose device init then fails.  Preloading torch's copy by path makes
+    libsva.so (and torch, whenever imported) bind that single runtime."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    cand = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(cand):
+        ct.CDLL(cand, mode=ct.RTLD_GLOBAL)
+
+
 def _load() -> ct.CDLL:
+    _preload_single_hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
@@ -111,6 +127,7 @@ def _load() -> ct.CDLL:
                                       dbl, dbl, vp, vp, vp]),
         "sva_ref_endpoints_d": (i32, [vp, i32, i32, P(Camera), P(Camera), i32, dbl, dbl, vp, vp]),
         "sva_disparity_to_depth_d": (i32, [vp, vp, i32, dbl, dbl, dbl, vp]),
+        "sva_disparity_to_depth": (i32, [vp, vp, i32, dbl, dbl, dbl, vp]),
         "sva_batch_sgm": (i32, [P(vp), i32, P(PairJob), i32, P(SgmParams)]),
     }
     for name, (res, args) in sig.items():
@@ -261,6 +278,13 @@ class Context:
     def ref_endpoints_d(self, W, H, cref, coth, k, t_near, t_far, ends, valid):
         self._chk(lib.sva_ref_endpoints_d(self.h, W, H, ct.byref(cref), ct.byref(coth), k,
                                           t_near, t_far, _ptr(ends), _ptr(valid)))
+
+    def disparity_to_depth(self, disp: np.ndarray, cam_distance, f, pixel_size):
+        d = np.ascontiguousarray(disp, dtype=np.uint8)
+        out = np.zeros(d.shape, np.float64)
+        self._chk(lib.sva_disparity_to_depth(self.h, _ptr(d), d.size, cam_distance, f, pixel_size,
+                                             _ptr(out)))
+        return out
 
     def disparity_to_depth_d(self, disp, n, cam_distance, f, pixel_size, depth):
         self._chk(lib.sva_disparity_to_depth_d(self.h, _ptr(disp), n, cam_distance, f,

@@ -527,6 +527,24 @@ int sva_disparity_to_depth_d(void* ctx, const uint8_t* disp, int n, double cam_d
     return SVA_OK;
 }
 
+int sva_disparity_to_depth(void* ctx, const uint8_t* disp, int n, double cam_distance, double f,
+                           double pixel_size, double* depth) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    if (!disp || !depth || n < 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
+    if (n == 0) return SVA_OK;
+    SVA_HIP(c, c->in_a.ensure((size_t)n), "staging");
+    SVA_HIP(c, c->out_a.ensure((size_t)n * 8), "staging");
+    SVA_HIP(c, hipMemcpyAsync(c->in_a.ptr, disp, (size_t)n, hipMemcpyHostToDevice, c->stream),
+            "upload");
+    SVA_HIP(c, launch_disp_to_depth(*c, (uint8_t*)c->in_a.ptr, n, cam_distance, f, pixel_size,
+                                    (double*)c->out_a.ptr), "depth launch");
+    SVA_HIP(c, hipMemcpyAsync(depth, c->out_a.ptr, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream),
+            "download");
+    SVA_HIP(c, hipStreamSynchronize(c->stream), "sync");
+    return SVA_OK;
+}
+
 // ---------------------------------------------------------------- batch --
 int sva_batch_sgm(void** ctxs, int n_ctx, const sva_pair_job* jobs, int n_jobs,
                   const sva_sgm_params* p) {

@@ -1,0 +1,121 @@
+// C++ host-mirror tests (include/sva.hpp).  Built by tests/test_host_cpp.py.
+//   ./test_host cpu   -- CPU-only checks (pair tables, bresenham, camera)
+//   ./test_host gpu   -- computeDisparity / computeDisparitySGM through the C-ABI
+#include <cstdio>
+#include <cstring>
+#include <random>
+
+#include "sva.hpp"
+
+static int failures = 0;
+#define CHECK(c)                                                        \
+    do {                                                                \
+        if (!(c)) {                                                     \
+            std::printf("FAIL %s:%d  %s\n", __FILE__, __LINE__, #c);    \
+            failures++;                                                 \
+        }                                                               \
+    } while (0)
+
+using namespace sva;
+
+static std::vector<Camera> rig(int W) {
+    // CameraStereoVision.cpp:24-39
+    std::vector<Camera> cams;
+    const double ps = 0.036 / W;
+    for (int y = 0; y < 5; y++)
+        for (int x = 0; x < 5; x++) cams.emplace_back(0.05, Point3d{-0.1 + x * 0.05, -0.1 + y * 0.05, -0.75}, ps);
+    return cams;
+}
+
+static void cpu_tests() {
+    auto cams = rig(640);
+    // getCameraPairs (functions.cpp:148-197)
+    CHECK(getCameraPairs(cams, MID_LEFT) == (std::vector<std::array<int, 2>>{{12, 11}}));
+    CHECK(getCameraPairs(cams, TO_CENTER).size() == 24);
+    CHECK(getCameraPairs(cams, TO_CENTER_SMALL).size() == 8);
+    CHECK(getCameraPairs(cams, LINE_VERTICAL) ==
+          (std::vector<std::array<int, 2>>{{12, 2}, {12, 7}, {12, 17}, {12, 22}}));
+    CHECK(getCameraPairs(cams, JUMP_CROSS)[3] == (std::array<int, 2>{12, 24}));
+    CHECK(getCameraPairs(cams, ORTHOGONAL).empty());
+    // CROSS with cameraNum (functions.cpp:199-213) keeps the reference quirks
+    auto q = getCameraPairs(cams, CROSS, 12);
+    CHECK(q == (std::vector<std::array<int, 2>>{{12, 7}, {12, 5}, {12, 11}, {12, 13}}));
+    auto fixed = getCameraPairs(cams, CROSS, 12, false);
+    CHECK(fixed == (std::vector<std::array<int, 2>>{{12, 7}, {12, 17}, {12, 11}, {12, 13}}));
+    CHECK(getCameraPairs(cams, CROSS, 5).size() == 2);   // 5-5 > 0 false, 5%5 == 0
+    auto groups = getGroups(cams, "CHESS");
+    CHECK(groups.size() == 13);
+    CHECK(getGroups(cams, "OTHER").empty());
+    // bresenham hand traces (same as tests/test_oracle_kat.py)
+    auto b = bresenham({5, 5}, {4, 9});
+    std::vector<Point2i> e{{5, 5}, {5, 6}, {5, 7}, {4, 8}, {4, 9}};
+    CHECK(b == e);
+    auto b2 = bresenham({3, 1}, {0, 0});
+    std::vector<Point2i> e2{{0, 0}, {1, 0}, {2, 1}, {3, 1}};
+    CHECK(b2 == e2);
+    // Camera::project truncates toward zero
+    Camera c(0.05, {0, 0, -0.75}, 0.036 / 640);
+    Point2i p = c.project({0.01, -0.02, 0.25});
+    CHECK(p.x == 8 && p.y == -17);
+    Camera u(12.0, {0, 0, 0}, 1.0);
+    Point3d v = u.inv_project({3, 4});
+    CHECK(v.x == 3.0 / 13 && v.y == 4.0 / 13 && v.z == 12.0 / 13);
+    // getAbsDiff on views
+    uint8_t a[4] = {0, 255, 10, 20}, bb[4] = {255, 0, 20, 10};
+    CHECK(getAbsDiff(ImageView(a, 2, 2), ImageView(bb, 2, 2)) == 530.0);
+    bool threw = false;
+    try { ImageView(a, 2, 2).roi(1, 1, 2, 2); } catch (const Error&) { threw = true; }
+    CHECK(threw);
+}
+
+static void gpu_tests() {
+    const int W = 192, H = 144;
+    auto cams = rig(W);
+    std::mt19937 rng(5);
+    std::vector<std::vector<uint8_t>> imgs(25, std::vector<uint8_t>(W * H));
+    for (auto& im : imgs)
+        for (auto& px : im) px = (uint8_t)(rng() & 255);
+    std::vector<ImageView> views;
+    for (auto& im : imgs) views.emplace_back(im.data(), W, H);
+    Engine eng(0);
+    auto pairs = getCameraPairs(cams, CROSS);
+    DisparityMaps m = computeDisparity(eng, views, cams, pairs, ImageView(), 8);
+    // each pair individually through the C-ABI, last pair wins (:55)
+    std::vector<uint8_t> d8(W * H, 0), val(W * H, 0);
+    std::vector<uint16_t> d16(W * H, 0);
+    for (auto& pr : pairs) {
+        sva_camera a = cams[pr[0]].abi(), b = cams[pr[1]].abi();
+        eng.check(sva_disparity_ref(eng.handle(), imgs[pr[0]].data(), imgs[pr[1]].data(), W, H, W,
+                                    nullptr, &a, &b, 8, 0.5, 1.0, d8.data(), d16.data(), val.data()));
+    }
+    CHECK(m.disp_u8 == d8 && m.disp_u16 == d16 && m.valid == val);
+    int nvalid = 0;
+    for (auto v : m.valid) nvalid += v;
+    CHECK(nvalid > W * H / 4);
+    auto depth = disparityToDepth(eng, m.disp_u8, cams[12], cams[11]);
+    CHECK(depth.size() == m.disp_u8.size());
+    // Mode S through the C++ layer
+    sva_sgm_params p;
+    sva_sgm_params_default(&p);
+    p.D = 64;
+    p.subpixel = 1;
+    std::vector<float> sub;
+    auto ds = computeDisparitySGM(eng, views[12], views[13], p, &sub);
+    CHECK(ds.size() == (size_t)W * H && sub.size() == ds.size());
+    bool threw = false;
+    try {
+        p.D = 50;
+        computeDisparitySGM(eng, views[12], views[13], p);
+    } catch (const Error& e) {
+        threw = e.status == SVA_ERR_UNSUPPORTED;
+    }
+    CHECK(threw);
+}
+
+int main(int argc, char** argv) {
+    const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
+    if (gpu) gpu_tests();
+    else cpu_tests();
+    std::printf("%s: %d failure(s)\n", gpu ? "gpu" : "cpu", failures);
+    return failures ? 1 : 0;
+}
