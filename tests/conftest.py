@@ -28,9 +28,15 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def ctx(sva):
+    """One context on cuda:0 that shares torch's current stream, so torch's
+    allocations/fills and the sva kernels are stream-ordered."""
     if sva.device_count() < 1:
         pytest.fail("GPU test selected but no HIP device is visible")
+    import torch
     c = sva.Context(0)
+    s = torch.cuda.Stream(torch.device("cuda:0"))
+    torch.cuda.set_stream(s)
+    c.set_stream(s.cuda_stream)
     yield c
     c.close()
 

@@ -61,8 +61,8 @@ def test_cost(ctx, sva, oracle, torch_dev, D, dir, dmin):
     cl, cr = oracle.census(L), oracle.census(R)
     C = torch.zeros((H, W, D), dtype=torch.uint8, device=torch_dev)
     p = sva.default_params(D=D, dmin=dmin, dir=dir)
-    ctx.cost_d(dev(cl.view(np.int64), torch_dev).data_ptr(),
-               dev(cr.view(np.int64), torch_dev).data_ptr(), W, H, p, C.data_ptr())
+    d_cl, d_cr = dev(cl.view(np.int64), torch_dev), dev(cr.view(np.int64), torch_dev)
+    ctx.cost_d(d_cl.data_ptr(), d_cr.data_ptr(), W, H, p, C.data_ptr())
     run_sync(ctx)
     assert np.array_equal(host(C), oracle.cost(cl, cr, D, dmin, dir))
 
@@ -71,7 +71,8 @@ def _paths(ctx, sva, torch_dev, C, P1=10, P2=120):
     H, W, D = C.shape
     L8 = torch.zeros((8, H, W, D), dtype=torch.uint8, device=torch_dev)
     p = sva.default_params(D=D, P1=P1, P2=P2)
-    ctx.paths_d(dev(C, torch_dev).data_ptr(), W, H, p, L8.data_ptr())
+    d_C = dev(C, torch_dev)
+    ctx.paths_d(d_C.data_ptr(), W, H, p, L8.data_ptr())
     run_sync(ctx)
     return host(L8)
 
@@ -113,7 +114,8 @@ def test_aggregate_sum(ctx, sva, oracle, torch_dev, D):
     rng = np.random.RandomState(D)
     C = rng.randint(0, 63, size=(H, W, D)).astype(np.uint8)
     S = torch.zeros((H, W, D), dtype=torch.int16, device=torch_dev)
-    ctx.aggregate_d(dev(C, torch_dev).data_ptr(), W, H, sva.default_params(D=D), S.data_ptr())
+    d_C = dev(C, torch_dev)
+    ctx.aggregate_d(d_C.data_ptr(), W, H, sva.default_params(D=D), S.data_ptr())
     run_sync(ctx)
     assert np.array_equal(host(S).view(np.uint16), oracle.aggregate(C))
 
@@ -132,7 +134,8 @@ def test_wta_first_minimum(ctx, sva, oracle, torch_dev, D):
     d = torch.zeros((H, W), dtype=torch.int16, device=torch_dev)
     s = torch.zeros((H, W), dtype=torch.float32, device=torch_dev)
     p = sva.default_params(D=D, dmin=dmin, subpixel=1)
-    ctx.wta_d(dev(S.view(np.int16), torch_dev).data_ptr(), W, H, p, d.data_ptr(), s.data_ptr())
+    d_S = dev(S.view(np.int16), torch_dev)
+    ctx.wta_d(d_S.data_ptr(), W, H, p, d.data_ptr(), s.data_ptr())
     run_sync(ctx)
     od, osub = oracle.wta(S, dmin)
     assert np.array_equal(host(d).view(np.uint16), od)
