@@ -35,6 +35,7 @@ WORKLOADS = {
     "4k_d256": dict(W=3840, H=2160, D=256),      # BASELINE configs[2]
     "1080p_d192": dict(W=1920, H=1080, D=192),   # BASELINE configs[4] per-pair shape
     "vga_d64": dict(W=640, H=480, D=64),         # BASELINE configs[0] shape
+    "1080half_d128": dict(W=1920, H=540, D=128), # experiment: C fits the Infinity Cache
 }
 
 

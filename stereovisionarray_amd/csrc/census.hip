@@ -15,9 +15,15 @@ constexpr int HX = 4, HY = 3;            // half window (9 wide, 7 high)
 constexpr int LW = TX + 2 * HX;          // 72 LDS columns
 constexpr int LH = TY + 2 * HY;          // 10 LDS rows
 
-__global__ __launch_bounds__(TX* TY) void census9x7_kernel(const uint8_t* __restrict__ img,
+// blockIdx.z selects the image: the left and right census of a pair are one
+// launch (img1/out1 may repeat img0/out0 for a single image).
+__global__ __launch_bounds__(TX* TY) void census9x7_kernel(const uint8_t* __restrict__ img0,
+                                                            const uint8_t* __restrict__ img1,
                                                             int W, int H, size_t pitch,
-                                                            uint64_t* __restrict__ out) {
+                                                            uint64_t* __restrict__ out0,
+                                                            uint64_t* __restrict__ out1) {
+    const uint8_t* __restrict__ img = blockIdx.z ? img1 : img0;
+    uint64_t* __restrict__ out = blockIdx.z ? out1 : out0;
     __shared__ uint8_t tile[LH][LW];
     const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
     const int tid = threadIdx.y * TX + threadIdx.x;
@@ -60,9 +66,18 @@ __global__ __launch_bounds__(TX* TY) void census9x7_kernel(const uint8_t* __rest
 hipError_t launch_census(Ctx& c, const uint8_t* img, int W, int H, size_t pitch,
                          uint64_t* out) {
     ScopedKernelTimer t(c, "census");
-    dim3 grid((W + TX - 1) / TX, (H + TY - 1) / TY);
-    hipLaunchKernelGGL(census9x7_kernel, grid, dim3(TX, TY), 0, c.stream, img, W, H, pitch,
-                       out);
+    dim3 grid((W + TX - 1) / TX, (H + TY - 1) / TY, 1);
+    hipLaunchKernelGGL(census9x7_kernel, grid, dim3(TX, TY), 0, c.stream, img, img, W, H, pitch,
+                       out, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_census_pair(Ctx& c, const uint8_t* left, const uint8_t* right, int W, int H,
+                              size_t pitch, uint64_t* out_l, uint64_t* out_r) {
+    ScopedKernelTimer t(c, "census");
+    dim3 grid((W + TX - 1) / TX, (H + TY - 1) / TY, 2);
+    hipLaunchKernelGGL(census9x7_kernel, grid, dim3(TX, TY), 0, c.stream, left, right, W, H,
+                       pitch, out_l, out_r);
     return hipGetLastError();
 }
 

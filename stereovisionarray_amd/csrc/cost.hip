@@ -14,11 +14,18 @@ namespace {
 constexpr int BLOCK = 256;
 constexpr int MAXW = 4096 / 64 + 256;  // LDS words for the smallest D (64): PX=64, +D
 
+// LDS word swizzle.  The D/16 lanes of one pixel read words 16 apart (one per
+// 16-disparity chunk): unswizzled that is a 4-way ds_read_b64 bank conflict at
+// D=128.  XOR-ing bits 0-2 of the word index with bits 4-6 (the chunk) spreads
+// the chunks of a pixel over 8 different bank pairs.  Bijective within each
+// aligned 128-word block, so MAXW rounded up to 128 words is enough.
+__device__ __forceinline__ int swz(int j) { return j ^ ((j >> 4) & 7); }
+
 __global__ __launch_bounds__(BLOCK) void hamming_cost_kernel(const uint64_t* __restrict__ cl,
                                                               const uint64_t* __restrict__ cr,
                                                               int W, int H, int D, int dmin,
                                                               int dir, uint8_t* __restrict__ C) {
-    __shared__ uint64_t rw[MAXW];
+    __shared__ uint64_t rw[(MAXW + 127) / 128 * 128];
     __shared__ uint8_t rvalid[MAXW];
     const int tpp = D / 16;                  // threads per pixel
     const int px_per_block = BLOCK / tpp;    // pixels per block
@@ -34,7 +41,7 @@ __global__ __launch_bounds__(BLOCK) void hamming_cost_kernel(const uint64_t* __r
         // dir = -1: word j <-> column x0 + px - 1 - dmin - j  (px-1-(x-x0)) + d = j
         int col = dir > 0 ? x0 + dmin + j : x0 + px_per_block - 1 - dmin - j;
         bool ok = col >= 0 && col < W;
-        rw[j] = ok ? cr[(size_t)y * W + col] : 0ull;
+        rw[swz(j)] = ok ? cr[(size_t)y * W + col] : 0ull;
         rvalid[j] = ok;
     }
     __syncthreads();
@@ -51,7 +58,7 @@ __global__ __launch_bounds__(BLOCK) void hamming_cost_kernel(const uint64_t* __r
         for (int b = 0; b < 4; b++) {
             const int d = d0 + q * 4 + b;
             const int j = dir > 0 ? lp + d : (px_per_block - 1 - lp) + d;
-            unsigned cst = rvalid[j] ? (unsigned)__popcll(l ^ rw[j]) : 62u;
+            unsigned cst = rvalid[j] ? (unsigned)__popcll(l ^ rw[swz(j)]) : 62u;
             w |= cst << (8 * b);
         }
         out[q] = w;

@@ -29,6 +29,8 @@
 #include "sva_device.h"
 #include "sva_internal.h"
 
+#include <cstdlib>
+
 namespace sva {
 namespace {
 
@@ -43,7 +45,23 @@ struct PathGeom {
     int blk_h;    // blocks per horizontal direction (H lines)
     int blk_w;    // blocks per vertical / diagonal direction (W lines)
     size_t vol;   // bytes of one direction volume (W*H*D)
+    int store_aux; // cache-policy bits for the path stores (0 = default)
 };
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+// Path volumes are written non-temporally (buffer aux bit nt = 2).  Measured
+// (1080p D=128): sgm_paths 0.807 -> 0.593 ms.  With default write-back stores
+// the 2.1 GB of L_r lines displace the 265 MB cost volume that all eight
+// directions re-read; streaming the stores keeps C cache-resident.
+constexpr int kStoreNT = 2;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, size_t bytes) {
+    // raw buffer: 32-bit byte offsets (every volume is < 4 GiB), hardware
+    // range check drops anything at or past `bytes`.
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                             (int)(unsigned)bytes, 0x00020000);
+}
 
 template <int NW>
 struct Words {
@@ -51,159 +69,199 @@ struct Words {
 };
 
 template <int NW>
-__device__ __forceinline__ Words<NW> load_words(const uint8_t* p) {
-    Words<NW> r;
+__device__ __forceinline__ Words<NW> bload(rsrc_t r, unsigned off) {
+    Words<NW> o;
     if constexpr (NW == 1) {
-        r.w[0] = *(const unsigned*)p;
+        o.w[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
     } else if constexpr (NW == 2) {
-        uint2 v = *(const uint2*)p;
-        r.w[0] = v.x; r.w[1] = v.y;
+        auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        o.w[0] = v[0]; o.w[1] = v[1];
     } else if constexpr (NW == 3) {
-        const unsigned* q = (const unsigned*)p;
-        r.w[0] = q[0]; r.w[1] = q[1]; r.w[2] = q[2];
+        auto v = __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, 0);
+        o.w[0] = v[0]; o.w[1] = v[1]; o.w[2] = v[2];
     } else {
-        uint4 v = *(const uint4*)p;
-        r.w[0] = v.x; r.w[1] = v.y; r.w[2] = v.z; r.w[3] = v.w;
+        auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+        o.w[0] = v[0]; o.w[1] = v[1]; o.w[2] = v[2]; o.w[3] = v[3];
     }
+    return o;
+}
+
+// VAR (ablation builds only, -DSVA_PATHS_ABLATION): 2 = no stores,
+// 3 = no loads, 4 = neither.  Production code is VAR = 0.
+template <int NW, int VAR>
+__device__ __forceinline__ void bstore(rsrc_t r, unsigned off, const unsigned (&w)[NW], int aux) {
+    if constexpr (VAR == 2 || VAR == 4) {
+#pragma unroll
+        for (int i = 0; i < NW; i++) asm volatile("" ::"v"(w[i]));
+    } else if constexpr (VAR == 9) {
+        typedef unsigned v2u __attribute__((ext_vector_type(2)));
+        switch (aux) {
+            case 2: __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, r, off, 0, 2); break;
+            case 16: __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, r, off, 0, 16); break;
+            case 18: __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, r, off, 0, 18); break;
+            case 17: __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, r, off, 0, 17); break;
+            default: __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, r, off, 0, 0); break;
+        }
+    } else if constexpr (NW == 1) {
+        __builtin_amdgcn_raw_buffer_store_b32(w[0], r, off, 0, kStoreNT);
+    } else if constexpr (NW == 2) {
+        typedef unsigned v2u __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, r, off, 0, kStoreNT);
+    } else if constexpr (NW == 3) {
+        typedef unsigned v3u __attribute__((ext_vector_type(3)));
+        __builtin_amdgcn_raw_buffer_store_b96((v3u){w[0], w[1], w[2]}, r, off, 0, kStoreNT);
+    } else {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128((v4u){w[0], w[1], w[2], w[3]}, r, off, 0, kStoreNT);
+    }
+}
+
+__device__ __forceinline__ unsigned add3(unsigned a, unsigned b, unsigned c) {
+    unsigned r;
+    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
 
-template <int NW>
-__device__ __forceinline__ void store_words(uint8_t* p, const unsigned (&w)[NW]) {
-    if constexpr (NW == 1) {
-        *(unsigned*)p = w[0];
-    } else if constexpr (NW == 2) {
-        *(uint2*)p = make_uint2(w[0], w[1]);
-    } else if constexpr (NW == 3) {
-        unsigned* q = (unsigned*)p;
-        q[0] = w[0]; q[1] = w[1]; q[2] = w[2];
-    } else {
-        *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-}
-
-// Cursor over one path line.  DIAG lines wrap in x and report the wrap.
+// Cursor over one path line: x and the byte offset of (x, y) in any
+// [H][W][D] volume (C and every L_r share the layout, so one offset serves
+// both the cost load and the path store).  Offsets advance by a constant
+// stride; DIAG lines wrap in x (offset -/+ W*D) and report the wrap.
 template <bool DIAG>
 struct Cursor {
-    int x, y;
-    __device__ __forceinline__ bool advance(int rx, int ry, int W) {
-        x += rx;
-        y += ry;
-        bool wrapped = false;
+    int x;
+    unsigned off;
+    __device__ __forceinline__ bool advance(int rx, unsigned stride, int W, unsigned WD) {
+        off += stride;
         if constexpr (DIAG) {
-            if (x >= W) { x -= W; wrapped = true; }
-            if (x < 0) { x += W; wrapped = true; }
+            x += rx;
+            const bool hi = x >= W, lo = x < 0;
+            x = hi ? x - W : (lo ? x + W : x);
+            off = hi ? off - WD : (lo ? off + WD : off);
+            return hi || lo;
         }
-        return wrapped;
-    }
-    __device__ __forceinline__ size_t off(int W, int D) const {
-        return ((size_t)y * (size_t)W + (size_t)x) * (size_t)D;
+        return false;
     }
 };
 
-// One recurrence step for the lane's DPL disparities.
+// One recurrence step for the lane's DPL disparities.  State A = L(q, .)
+// (unnormalised u16 pairs), m = min_k L(q, k) broadcast over the row.
+//   u      = min(min(A(d-1), A(d+1)) + P1, A(d), m + P2)      (all >= m)
+//   L(p,d) = u + C(p,d) - m  = v_add3_u32(u, c, -(m * 0x10001))
+// The add3 is exact per 16-bit half: u_lo >= m makes the low half carry
+// exactly once, which the high half's (0xffff - m) absorbs.
 template <int DPL>
-__device__ __forceinline__ void sgm_step(const unsigned (&cw)[DPL / 4], unsigned (&B)[DPL / 2],
-                                         unsigned (&ow)[DPL / 4], unsigned P1, unsigned P2) {
+__device__ __forceinline__ void sgm_step(const unsigned (&cw)[DPL / 4], unsigned (&A)[DPL / 2],
+                                         unsigned& m, unsigned (&ow)[DPL / 4], unsigned P1,
+                                         unsigned P2) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
     unsigned c[NP];
 #pragma unroll
     for (int w = 0; w < NW; w++) unpack4(cw[w], c[2 * w], c[2 * w + 1]);
     // neighbours: X = lane k-1's last pair, Y = lane k+1's first pair
-    const unsigned X = row_shr1(B[NP - 1], INF2);
-    const unsigned Y = row_shl1(B[0], INF2);
+    const unsigned X = row_shr1(A[NP - 1], INF2);
+    const unsigned Y = row_shl1(A[0], INF2);
     unsigned M[NP];
-    M[0] = __builtin_amdgcn_alignbit(B[0], X, 16);
+    M[0] = __builtin_amdgcn_alignbit(A[0], X, 16);
 #pragma unroll
-    for (int j = 1; j < NP; j++) M[j] = __builtin_amdgcn_alignbit(B[j], B[j - 1], 16);
-    const unsigned Qlast = __builtin_amdgcn_alignbit(Y, B[NP - 1], 16);
-    unsigned Ln[NP];
+    for (int j = 1; j < NP; j++) M[j] = __builtin_amdgcn_alignbit(A[j], A[j - 1], 16);
+    const unsigned Qlast = __builtin_amdgcn_alignbit(Y, A[NP - 1], 16);
+    const unsigned mP2 = m + P2;
+    const unsigned K = 0u - (m | (m << 16));
 #pragma unroll
     for (int j = 0; j < NP; j++) {
         const u16x2 q = as_v2(j < NP - 1 ? M[j + 1] : Qlast);
         u16x2 t = vmin2(as_v2(M[j]), q) + splat2(P1);
-        t = vmin2(t, as_v2(B[j]));
-        t = vmin2(t, splat2(P2));
-        Ln[j] = as_u32(t + as_v2(c[j]));
+        t = vmin2(t, as_v2(A[j]));
+        t = vmin2(t, splat2(mP2));
+        A[j] = add3(as_u32(t), c[j], K);
     }
 #pragma unroll
-    for (int w = 0; w < NW; w++) ow[w] = pack4(Ln[2 * w], Ln[2 * w + 1]);
-    // m = min_k L over the 16-lane row, then normalise the carried state
-    u16x2 mm = as_v2(Ln[0]);
+    for (int w = 0; w < NW; w++) ow[w] = pack4(A[2 * w], A[2 * w + 1]);
+    u16x2 mm = as_v2(A[0]);
 #pragma unroll
-    for (int j = 1; j < NP; j++) mm = vmin2(mm, as_v2(Ln[j]));
-    unsigned m = mm.x < mm.y ? mm.x : mm.y;
-    m = row_min_u32(m);
-#pragma unroll
-    for (int j = 0; j < NP; j++) B[j] = as_u32(as_v2(Ln[j]) - splat2(m));
+    for (int j = 1; j < NP; j++) mm = vmin2(mm, as_v2(A[j]));
+    m = row_min_u32(mm.x < mm.y ? mm.x : mm.y);
 }
 
-template <int DPL, bool DIAG>
-__device__ __forceinline__ void path_line(const uint8_t* __restrict__ C, uint8_t* __restrict__ L,
-                                          const PathGeom& g, int rx, int ry, int line, int k) {
+template <int DPL, bool DIAG, int VAR>
+__device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& g, int rx, int ry,
+                                          int line, int k) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
     const int W = g.W, H = g.H, D = g.D;
     const unsigned P1 = (unsigned)g.P1, P2 = (unsigned)g.P2;
     const int steps = ry == 0 ? W : H;
+    const unsigned WD = (unsigned)W * (unsigned)D;
+    const unsigned stride = (unsigned)((ry * W + rx) * D);
+    int x0, y0;
+    if (ry == 0) { y0 = line; x0 = rx > 0 ? 0 : W - 1; }
+    else { y0 = ry > 0 ? 0 : H - 1; x0 = line; }
     Cursor<DIAG> cc;
-    if (ry == 0) { cc.y = line; cc.x = rx > 0 ? 0 : W - 1; }
-    else { cc.y = ry > 0 ? 0 : H - 1; cc.x = line; }
-    Cursor<DIAG> pc = cc;        // prefetch cursor, clamped at the last step
-    int tp = 0;
-    const uint8_t* Cb = C + k * DPL;
-    uint8_t* Lb = L + k * DPL;
+    cc.x = x0;
+    cc.off = ((unsigned)y0 * (unsigned)W + (unsigned)x0) * (unsigned)D + (unsigned)(k * DPL);
+    // Prefetch cursor: runs PF steps ahead and may run past the line's end;
+    // those loads land in-range garbage or, past the volume, the buffer range
+    // check returns 0 -- never consumed either way.
+    Cursor<DIAG> pc = cc;
 
-    unsigned B[NP];
+    unsigned A[NP];
 #pragma unroll
-    for (int j = 0; j < NP; j++) B[j] = 0u;   // L(q) = 0, m = 0  =>  L = C
+    for (int j = 0; j < NP; j++) A[j] = 0u;   // L(q) = 0, m = 0  =>  L = C
+    unsigned m = 0u;
 
     Words<NW> ring[PF];
 #pragma unroll
     for (int p = 0; p < PF; p++) {
-        ring[p] = load_words<NW>(Cb + pc.off(W, D));
-        if (tp < steps - 1) { pc.advance(rx, ry, W); tp++; }
+        if constexpr (VAR == 3 || VAR == 4) {
+#pragma unroll
+            for (int w = 0; w < NW; w++) ring[p].w[w] = (0x05030201u * (unsigned)(p + 1) + (unsigned)k) & 0x1f1f1f1fu;
+        } else {
+            ring[p] = bload<NW>(rC, pc.off);
+        }
+        pc.advance(rx, stride, W, WD);
     }
+
+    // One step consumes ring slot p in place (loaded PF steps ago) and only
+    // then refills that slot with the load for step t+PF, so the old and new
+    // values never overlap and the slot keeps its registers: no copies, and
+    // every wait is for a load issued ~PF steps earlier.  (Refilling first
+    // made hipcc copy the whole ring at the loop head behind vmcnt(1..3).)
+    auto step = [&](int p, bool refill) {
+        unsigned cw[NW];
+#pragma unroll
+        for (int w = 0; w < NW; w++) cw[w] = ring[p].w[w];
+        unsigned ow[NW];
+        sgm_step<DPL>(cw, A, m, ow, P1, P2);
+        bstore<NW, VAR>(rL, cc.off, ow, g.store_aux);
+        const bool wrapped = cc.advance(rx, stride, W, WD);
+        if constexpr (DIAG) {
+            if (wrapped) {
+#pragma unroll
+                for (int j = 0; j < NP; j++) A[j] = 0u;
+                m = 0u;
+            }
+        }
+        if (refill) {
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (VAR == 3 || VAR == 4) {
+#pragma unroll
+                for (int w = 0; w < NW; w++) ring[p].w[w] = (cw[w] * 3u + (unsigned)p) & 0x1f1f1f1fu;
+            } else {
+                ring[p] = bload<NW>(rC, pc.off);
+            }
+            pc.advance(rx, stride, W, WD);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
 
     int t = 0;
     for (; t + PF <= steps; t += PF) {
 #pragma unroll
-        for (int p = 0; p < PF; p++) {
-            unsigned cw[NW];
-#pragma unroll
-            for (int w = 0; w < NW; w++) cw[w] = ring[p].w[w];
-            ring[p] = load_words<NW>(Cb + pc.off(W, D));
-            if (tp < steps - 1) { pc.advance(rx, ry, W); tp++; }
-            unsigned ow[NW];
-            sgm_step<DPL>(cw, B, ow, P1, P2);
-            store_words<NW>(Lb + cc.off(W, D), ow);
-            const bool wrapped = cc.advance(rx, ry, W);
-            if constexpr (DIAG) {
-                if (wrapped) {
-#pragma unroll
-                    for (int j = 0; j < NP; j++) B[j] = 0u;
-                }
-            }
-        }
+        for (int p = 0; p < PF; p++) step(p, true);
     }
     // tail: fewer than PF steps left, all already in the ring
 #pragma unroll
-    for (int p = 0; p < PF; p++) {
-        if (t + p < steps) {
-            unsigned cw[NW];
-#pragma unroll
-            for (int w = 0; w < NW; w++) cw[w] = ring[p].w[w];
-            unsigned ow[NW];
-            sgm_step<DPL>(cw, B, ow, P1, P2);
-            store_words<NW>(Lb + cc.off(W, D), ow);
-            const bool wrapped = cc.advance(rx, ry, W);
-            if constexpr (DIAG) {
-                if (wrapped) {
-#pragma unroll
-                    for (int j = 0; j < NP; j++) B[j] = 0u;
-                }
-            }
-        }
-    }
+    for (int p = 0; p < PF; p++)
+        if (t + p < steps) step(p, false);
 }
 
 // Direction table, identical to oracle svo_direction().
@@ -213,16 +271,17 @@ __device__ __forceinline__ void dir_of(int r, int& rx, int& ry) {
     ry = T[r][1];
 }
 
-template <int DPL>
+template <int DPL, int VAR = 0>
 __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __restrict__ C,
                                                                uint8_t* __restrict__ L8,
                                                                PathGeom g) {
     // Horizontal directions (W steps per line, the longest) get the lowest
-    // block ids so they are dispatched first; the rest follow.
+    // block ids and issue priority so they are never the tail.
     int b = blockIdx.x, r, lb;
     if (b < 2 * g.blk_h) {
         r = b / g.blk_h;
         lb = b - r * g.blk_h;
+        __builtin_amdgcn_s_setprio(1);
     } else {
         b -= 2 * g.blk_h;
         r = 2 + b / g.blk_w;
@@ -234,9 +293,10 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
     if (line >= nlines) return;  // whole 16-lane row leaves together
     int rx, ry;
     dir_of(r, rx, ry);
-    uint8_t* L = L8 + (size_t)r * g.vol;
-    if (r >= 4) path_line<DPL, true>(C, L, g, rx, ry, line, k);
-    else path_line<DPL, false>(C, L, g, rx, ry, line, k);
+    const rsrc_t rC = make_rsrc(C, g.vol);
+    const rsrc_t rL = make_rsrc(L8 + (size_t)r * g.vol, g.vol);
+    if (r >= 4) path_line<DPL, true, VAR>(rC, rL, g, rx, ry, line, k);
+    else path_line<DPL, false, VAR>(rC, rL, g, rx, ry, line, k);
 }
 
 }  // namespace
@@ -251,7 +311,31 @@ hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, i
     g.blk_h = (H + LINES_PER_BLOCK - 1) / LINES_PER_BLOCK;
     g.blk_w = (W + LINES_PER_BLOCK - 1) / LINES_PER_BLOCK;
     g.vol = (size_t)W * H * D;
+    g.store_aux = 0;
+    if (g.vol >= (size_t)1 << 32) return hipErrorInvalidValue;  // 32-bit buffer offsets
     dim3 grid(2 * g.blk_h + 6 * g.blk_w);
+#ifdef SVA_PATHS_ABLATION
+    static int var = getenv("SVA_PATHS_VARIANT") ? atoi(getenv("SVA_PATHS_VARIANT")) : 0;
+    if (D == 128 && var > 0) {
+        switch (var) {
+            case 2: hipLaunchKernelGGL((sgm_paths_kernel<8, 2>), grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
+            case 3: hipLaunchKernelGGL((sgm_paths_kernel<8, 3>), grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
+            case 4: hipLaunchKernelGGL((sgm_paths_kernel<8, 4>), grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
+            case 9: case 10: case 11: case 12: {
+                static const int auxv[4] = {2, 16, 18, 17};
+                g.store_aux = auxv[var - 9];
+                hipLaunchKernelGGL((sgm_paths_kernel<8, 9>), grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break; }
+            case 5: hipLaunchKernelGGL((sgm_paths_kernel<8, 4>), dim3(2 * g.blk_h), dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
+            case 6: { PathGeom g2 = g; g2.blk_h = 0;   // vertical + diagonal only (r = 2..7)
+                      hipLaunchKernelGGL((sgm_paths_kernel<8, 4>), dim3(6 * g.blk_w), dim3(PATH_BLOCK), 0, c.stream, C, L8, g2); break; }
+            case 7: hipLaunchKernelGGL((sgm_paths_kernel<8, 0>), dim3(2 * g.blk_h), dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
+            case 8: { PathGeom g2 = g; g2.blk_h = 0;
+                      hipLaunchKernelGGL((sgm_paths_kernel<8, 0>), dim3(6 * g.blk_w), dim3(PATH_BLOCK), 0, c.stream, C, L8, g2); break; }
+            default: break;
+        }
+        return hipGetLastError();
+    }
+#endif
     switch (D) {
         case 64: hipLaunchKernelGGL(sgm_paths_kernel<4>, grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
         case 128: hipLaunchKernelGGL(sgm_paths_kernel<8>, grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;

@@ -161,8 +161,7 @@ int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int
     uint64_t* cr = (uint64_t*)c->census_r.ptr;
     uint8_t* C = (uint8_t*)c->cost.ptr;
     uint8_t* L8 = (uint8_t*)c->paths.ptr;
-    SVA_HIP(c, launch_census(*c, left, W, H, pitch, cl), "census launch");
-    SVA_HIP(c, launch_census(*c, right, W, H, pitch, cr), "census launch");
+    SVA_HIP(c, launch_census_pair(*c, left, right, W, H, pitch, cl, cr), "census launch");
     SVA_HIP(c, launch_cost(*c, cl, cr, W, H, p->D, p->dmin, p->dir, C), "cost launch");
     SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
     SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, disp, sub), "wta launch");

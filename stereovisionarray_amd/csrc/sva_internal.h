@@ -77,6 +77,8 @@ struct ScopedKernelTimer {
 
 // census.hip
 hipError_t launch_census(Ctx& c, const uint8_t* img, int W, int H, size_t pitch, uint64_t* out);
+hipError_t launch_census_pair(Ctx& c, const uint8_t* left, const uint8_t* right, int W, int H,
+                              size_t pitch, uint64_t* out_l, uint64_t* out_r);
 // cost.hip
 hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,
                        int dmin, int dir, uint8_t* C);

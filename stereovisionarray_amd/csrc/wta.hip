@@ -10,6 +10,8 @@
 #include "sva_device.h"
 #include "sva_internal.h"
 
+#include <cstdlib>
+
 namespace sva {
 namespace {
 
@@ -40,6 +42,28 @@ __device__ __forceinline__ void load_nw(const uint8_t* p, unsigned (&w)[NW]) {
     }
 }
 
+#ifdef SVA_PATHS_ABLATION
+__constant__ int g_wta_nt = 1;
+#endif
+
+// Last-use reads of the path volumes: non-temporal (ablation: SVA_WTA_NT=0).
+template <int NW>
+__device__ __forceinline__ void load_nw_nt(const uint8_t* p, unsigned (&w)[NW]) {
+    const unsigned* q = (const unsigned*)p;
+    if constexpr (NW == 2) {
+        typedef unsigned v2u __attribute__((ext_vector_type(2)));
+        v2u v = __builtin_nontemporal_load((const v2u*)q);
+        w[0] = v[0]; w[1] = v[1];
+    } else if constexpr (NW == 4) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        v4u v = __builtin_nontemporal_load((const v4u*)q);
+        w[0] = v[0]; w[1] = v[1]; w[2] = v[2]; w[3] = v[3];
+    } else {
+#pragma unroll
+        for (int i = 0; i < NW; i++) w[i] = __builtin_nontemporal_load(q + i);
+    }
+}
+
 // S pairs for this lane from the 8 direction volumes.
 template <int DPL>
 __device__ __forceinline__ void sum_paths(const uint8_t* p, size_t vol, unsigned (&S)[DPL / 2]) {
@@ -47,8 +71,18 @@ __device__ __forceinline__ void sum_paths(const uint8_t* p, size_t vol, unsigned
 #pragma unroll
     for (int j = 0; j < NP; j++) S[j] = 0u;
     unsigned w[8][NW];
+#ifdef SVA_PATHS_ABLATION
+    if (g_wta_nt) {
 #pragma unroll
-    for (int r = 0; r < 8; r++) load_nw<NW>(p + (size_t)r * vol, w[r]);
+        for (int r = 0; r < 8; r++) load_nw_nt<NW>(p + (size_t)r * vol, w[r]);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 8; r++) load_nw<NW>(p + (size_t)r * vol, w[r]);
+    }
+#else
+#pragma unroll
+    for (int r = 0; r < 8; r++) load_nw_nt<NW>(p + (size_t)r * vol, w[r]);
+#endif
 #pragma unroll
     for (int r = 0; r < 8; r++)
 #pragma unroll
@@ -170,6 +204,14 @@ __global__ void lr_check_kernel(uint16_t* __restrict__ dl, const uint16_t* __res
 
 hipError_t launch_wta_from_paths(Ctx& c, const uint8_t* L8, int W, int H, int D, int dmin,
                                  uint16_t* disp, float* sub) {
+#ifdef SVA_PATHS_ABLATION
+    static int once = [] {
+        int v = getenv("SVA_WTA_NT") ? atoi(getenv("SVA_WTA_NT")) : 1;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wta_nt), &v, sizeof(int));
+        return 0;
+    }();
+    (void)once;
+#endif
     ScopedKernelTimer t(c, "wta");
     const int npix = W * H;
     const size_t vol = (size_t)npix * D;
