@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--pairs-per-rank", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=1)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (real runs); gloo = rehearsal with ranks "
+                         "sharing one GPU, maps gathered through host memory")
     return ap.parse_args()
 
 
@@ -89,6 +92,7 @@ def main():
     import torch
     import torch.distributed as dist
     import stereovisionarray_amd as sva
+    from stereovisionarray_amd import dist as sdist
     from stereovisionarray_amd import synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -99,11 +103,16 @@ def main():
             raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
+    ndev = torch.cuda.device_count()
+    local = local % ndev if a.dist_backend == "gloo" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     wl = WORKLOADS[a.workload]
     W, H, D = wl["W"], wl["H"], wl["D"]
@@ -115,22 +124,24 @@ def main():
     ctx.set_stream(stream.cuda_stream)
     ctx.reserve(W, H, D)
 
+    n_units = world * P   # unit u = pair u, owned by rank u mod world (sdist.shard)
     lefts, rights = [], []
-    for j in range(P):
-        L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=1 + rank * P + j)
+    for u in sdist.shard(n_units, rank, world):
+        L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=1 + u)
         lefts.append(torch.from_numpy(L).to(dev))
         rights.append(torch.from_numpy(R).to(dev))
     disp = torch.zeros((P, H, W), dtype=torch.int16, device=dev)
     sub = torch.zeros((P, H, W), dtype=torch.float32, device=dev)
-    gathered = (torch.zeros((world, P, H, W), dtype=torch.int16, device=dev)
-                if world > 1 and rank == 0 else None)
 
     def step():
         for j in range(P):
             ctx.disparity_sgm_d(lefts[j].data_ptr(), rights[j].data_ptr(), W, H, W, params,
                                 disp[j].data_ptr(), sub[j].data_ptr())
-        if world > 1:   # the path's one exchange: disparity maps -> rank 0
-            dist.gather(disp, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+        if world > 1:   # the path's one exchange: disparity maps -> rank 0 (RCCL)
+            if a.dist_backend == "nccl":
+                sdist.gather_maps(disp, n_units, dst=0)
+            else:
+                sdist.gather_maps(disp.cpu(), n_units, dst=0)
 
     for _ in range(a.warmup):
         step()
@@ -150,7 +161,8 @@ def main():
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if a.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
