@@ -36,7 +36,14 @@ WORKLOADS = {
     "1080p_d192": dict(W=1920, H=1080, D=192),   # BASELINE configs[4] per-pair shape
     "vga_d64": dict(W=640, H=480, D=64),         # BASELINE configs[0] shape
     "1080half_d128": dict(W=1920, H=540, D=128), # experiment: C fits the Infinity Cache
+    # BASELINE configs[3]: 8-camera array (2x4 grid), all 28 pairwise baselines,
+    # pairs sharded over ranks, gather + per-reference-camera median fusion
+    "array8": dict(W=1920, H=1080, D=128, array=(2, 4)),
 }
+
+ARRAY_PITCH = 0.05             # m between grid neighbours (CameraStereoVision.cpp:34-39)
+ARRAY_F = 0.05                 # m
+ARRAY_PS = 0.036 / 1920        # m / pixel
 
 
 def parse():
@@ -87,6 +94,176 @@ def load_traffic(workload):
         return None
 
 
+def timed(a, step, world, dev, ctx):
+    """W untimed steps, then exactly K steps between barrier + synchronize,
+    max over ranks."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if a.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def kernel_table(ctx, names=("census", "cost", "sgm_paths", "wta", "fuse_depth")):
+    kernels = {}
+    for name in names:
+        ms, n = ctx.kernel_time(name)
+        if n:
+            kernels[name] = {"avg_ms": ms / n, "launches": n}
+    return kernels
+
+
+def roofline_of(kernels, W, H, D, workload):
+    agg = kernels.get("sgm_paths")
+    if not agg:
+        return None
+    alg_bytes = AGG_BYTES_PER_DISP * W * H * D
+    achieved = alg_bytes / (agg["avg_ms"] * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": load_traffic(workload),
+            "kernel": "sgm_paths", "kernel_avg_ms": round(agg["avg_ms"], 4),
+            "alg_bytes_per_launch": alg_bytes}
+
+
+def run_array(a, wl, world, rank, local, dev):
+    """BASELINE configs[3]: an 8-camera array (2x4 grid), all 28 pairwise
+    baselines at 1080p D=128.  Pair u (grouped by reference camera) is matched
+    by rank u mod N along its own baseline step; the u16 maps
+    are gathered to rank 0 (RCCL), which fuses, per reference camera, the
+    median depth over that camera's pairs.  Total work is
+    fixed (strong scaling)."""
+    import torch
+    import torch.distributed as dist
+    import stereovisionarray_amd as sva
+    from stereovisionarray_amd import dist as sdist
+    from stereovisionarray_amd import synth
+
+    W, H, D = wl["W"], wl["H"], wl["D"]
+    rows, cols = wl["array"]
+    grid = synth.array_grid(rows, cols)
+    pairs = synth.array_pairs(len(grid))
+    n_units = len(pairs)
+    kmax = max(synth.pair_step(grid[i], grid[j])[2] for i, j in pairs)
+    dmax = (D - 1) // kmax
+    delta = synth.array_delta(H, W, dmax)
+    views_np = synth.array_views(H, W, grid, delta, seed=7)
+
+    ctx = sva.Context(local)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
+    ctx.reserve(W, H, D)
+    mine = sdist.shard(n_units, rank, world)
+    need = sorted({c for u in mine for c in pairs[u]})
+    views = {c: torch.from_numpy(views_np[c]).to(dev) for c in need}
+    jobs = []
+    for u in mine:
+        i, j = pairs[u]
+        sx, sy, _ = synth.pair_step(grid[i], grid[j])
+        jobs.append((views[i], views[j], sva.default_params(D=D, dmin=0, dir=sx, dir_y=sy)))
+    disp = torch.zeros((len(mine), H, W), dtype=torch.int16, device=dev)
+    # fusion groups on rank 0: reference camera i owns pairs [off, off + n)
+    groups, off = [], 0
+    for i in range(len(grid)):
+        n = sum(1 for p in pairs if p[0] == i)
+        if n:
+            bases = [synth.pair_step(grid[i], grid[j])[2] * ARRAY_PITCH
+                     for (ii, j) in pairs[off:off + n]]
+            groups.append((i, off, n, bases))
+        off += n
+    depth = torch.zeros((len(groups), H, W), dtype=torch.float64, device=dev)
+    nvalid = torch.zeros((len(groups), H, W), dtype=torch.uint8, device=dev)
+    maps = {"all": None}
+
+    def step():
+        for jb, (L, R, p) in enumerate(jobs):
+            ctx.disparity_sgm_d(L.data_ptr(), R.data_ptr(), W, H, W, p, disp[jb].data_ptr())
+        if world > 1:
+            if a.dist_backend == "nccl":
+                allm = sdist.gather_maps(disp, n_units, dst=0)
+            else:
+                allm = sdist.gather_maps(disp.cpu(), n_units, dst=0)
+                allm = allm.to(dev) if allm is not None else None
+        else:
+            allm = disp
+        if rank == 0:
+            for g, (i, o, n, bases) in enumerate(groups):
+                ctx.fuse_depth_d(allm[o].data_ptr(), n, W, H, bases, ARRAY_F, ARRAY_PS, 0xFFFF,
+                                 depth[g].data_ptr(), nvalid[g].data_ptr())
+            maps["all"] = allm
+
+    elapsed = timed(a, step, world, dev, ctx)
+    kernels = kernel_table(ctx)
+    value = n_units * W * H * D * a.steps / elapsed / 1e6
+    out = None
+    if rank == 0:
+        # sanity: camera 0 sees the texture unwarped, so its fused depth must be
+        # the stripe-plane depth pitch*f/(delta*ps) away from stripe edges
+        z0 = depth[0].cpu().numpy()
+        truth = ARRAY_PITCH * ARRAY_F / (delta * ARRAY_PS)
+        edge = np.zeros(W, bool)
+        cuts = np.flatnonzero(np.diff(delta[0]) != 0)
+        for c in cuts:
+            edge[max(0, c - D): c + D] = True
+        inner = np.zeros((H, W), bool)
+        inner[D:H - D, D:W - D] = True
+        inner &= ~edge[None, :]
+        exact = float(np.mean(np.abs(z0[inner] - truth[inner]) <= 1e-9 * truth[inner]))
+        out = {
+            "metric": "Mdisparities/sec (W·H·D/s), 8-camera array, all 28 pairwise "
+                      "baselines, 1080p D=128, gather + fuse",
+            "value": round(value, 1),
+            "unit": "Mdisp/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u16",
+            "data": "synthetic 2x4 array views of one MT19937 texture warped by 12 "
+                    f"stripe planes (per-grid-unit disparity 4..{dmax} px)",
+            "config": {"workload": f"array8: 2x4 grid, {n_units} pairs {W}x{H} D={D} Mode S "
+                                   "along each pair's baseline step, RCCL gather, per-camera "
+                                   "median fusion on rank 0",
+                       "W": W, "H": H, "D": D, "P1": 10, "P2": 120, "pairs": n_units,
+                       "parallelism": f"pairs sharded over {world} rank(s), gather to rank 0"},
+            "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
+            "fused_maps_per_s": round(len(groups) * a.steps / elapsed, 2),
+            "cam0_interior_depth_exact_frac": round(exact, 4),
+            "roofline": roofline_of(kernels, W, H, D, "1080p_d128"),
+            "cpu_baseline": None,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(W, H, D, a.cpu_threads)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     import torch
@@ -116,6 +293,8 @@ def main():
 
     wl = WORKLOADS[a.workload]
     W, H, D = wl["W"], wl["H"], wl["D"]
+    if "array" in wl:
+        return run_array(a, wl, world, rank, local, dev)
     P = a.pairs_per_rank
     params = sva.default_params(D=D, dmin=0, dir=-1, subpixel=1)
     ctx = sva.Context(local)
@@ -143,34 +322,8 @@ def main():
             else:
                 sdist.gather_maps(disp.cpu(), n_units, dst=0)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ctx.set_timing(True)
-    ctx.reset_timing()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    ctx.set_timing(False)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=dev if a.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    kernels = {}
-    for name in ("census", "cost", "sgm_paths", "wta"):
-        ms, n = ctx.kernel_time(name)
-        if n:
-            kernels[name] = {"avg_ms": ms / n, "launches": n}
+    elapsed = timed(a, step, world, dev, ctx)
+    kernels = kernel_table(ctx)
     # sanity: the result is a real disparity map (exact on the stripe interiors)
     d0 = disp[0].cpu().numpy().view(np.uint16)
     assert d0.max() < D, "disparity out of range"
@@ -179,16 +332,7 @@ def main():
     disparities = units * W * H * D
     value = disparities / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1e3
-    agg = kernels.get("sgm_paths")
-    roofline = None
-    if agg:
-        alg_bytes = AGG_BYTES_PER_DISP * W * H * D
-        achieved = alg_bytes / (agg["avg_ms"] * 1e-3) / 1e9
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": load_traffic(a.workload),
-                    "kernel": "sgm_paths", "kernel_avg_ms": round(agg["avg_ms"], 4),
-                    "alg_bytes_per_launch": alg_bytes}
+    roofline = roofline_of(kernels, W, H, D, a.workload)
     out = {
         "metric": "Mdisparities/sec (W·H·D/s) at 1080p D=128" if a.workload == "1080p_d128"
                   else f"Mdisparities/sec (W·H·D/s) {a.workload}",

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SVA_ABI_VERSION 1
+#define SVA_ABI_VERSION 2
 
 enum {
     SVA_OK = 0,
@@ -55,7 +55,9 @@ typedef struct sva_camera {
 typedef struct sva_sgm_params {
     int32_t D;           /* disparity count; GPU path: multiple of 32, 32..256     */
     int32_t dmin;        /* first disparity                                        */
-    int32_t dir;         /* +1: match at x+(dmin+d) in the other image, -1: x-(..) */
+    int32_t dir;         /* x component of the match step: +1: x+(dmin+d) in the
+                            other image, -1: x-(dmin+d) (rectified horizontal);
+                            see dir_y for array baselines                          */
     int32_t P1;          /* small-jump penalty (default 10)                        */
     int32_t P2;          /* large-jump penalty (default 120); 0 <= P1, P2 <= 193    */
     int32_t subpixel;    /* 1: also write the f32 parabola sub-pixel map          */
@@ -63,6 +65,12 @@ typedef struct sva_sgm_params {
     int32_t lr_max_diff; /* max |dL - dR| kept by the check (default 1)            */
     uint16_t invalid;    /* disparity written for pixels the check rejects         */
     uint16_t _pad;
+    int32_t dir_y;       /* y component (default 0).  (dir, dir_y) = integer
+                            baseline direction of an array pair, |comp| <= 255:
+                            disparity s = dmin+d counts pixels along the major
+                            axis, the minor offset is round_half_up(s*m/M)
+                            (DESIGN.md §2.2); (+-1,0), (0,+-1), (+-1,+-1) are the
+                            horizontal / vertical / 45-degree cases              */
 } sva_sgm_params;
 
 /* One stereo pair for the batch API. */
@@ -142,6 +150,18 @@ int sva_disparity_ref_d(void* ctx, const uint8_t* ref_img, const uint8_t* other_
 int sva_ref_endpoints_d(void* ctx, int width, int height, const sva_camera* ref_cam,
                         const sva_camera* other_cam, int k, double t_near, double t_far,
                         int32_t* ends, uint8_t* valid);
+
+/* Multi-pair depth fusion on the root: per
+ * pixel the median of baseline_i * f / (disp_i * pixel_size) over the maps
+ * with disp_i != invalid and disp_i > 0 (mean of the middle two for an even
+ * count), 0 if none.  disps: [n_maps][H][W] u16 (device / host), baselines:
+ * HOST array of n_maps per-axis baselines (m), n_maps <= 32; n_valid nullable. */
+int sva_fuse_depth_d(void* ctx, const uint16_t* disps, int n_maps, int width, int height,
+                     const double* baselines, double f, double pixel_size, uint16_t invalid,
+                     double* depth, uint8_t* n_valid);
+int sva_fuse_depth(void* ctx, const uint16_t* disps, int n_maps, int width, int height,
+                   const double* baselines, double f, double pixel_size, uint16_t invalid,
+                   double* depth, uint8_t* n_valid);
 
 /* Disparity -> depth, CameraStereoVision.cpp:47,98-100 (f64; 0 where disp 0). */
 int sva_disparity_to_depth_d(void* ctx, const uint8_t* disp, int n, double cam_distance,

@@ -50,6 +50,9 @@ def _load():
         "svo_disp_to_depth": (None, [vp, i32, dbl, dbl, dbl, vp]),
         "svo_census": (None, [vp, i32, i32, ct.c_ssize_t, vp]),
         "svo_cost": (None, [vp, vp, i32, i32, i32, i32, i32, vp]),
+        "svo_cost2": (None, [vp, vp, i32, i32, i32, i32, i32, i32, vp]),
+        "svo_lr_check2": (None, [vp, vp, i32, i32, i32, i32, i32, ct.c_uint16]),
+        "svo_fuse_depth": (None, [vp, i32, i32, i32, vp, dbl, dbl, ct.c_uint16, vp, vp]),
         "svo_path": (None, [vp, i32, i32, i32, i32, i32, i32, i32, vp]),
         "svo_direction": (None, [i32, P(i32), P(i32)]),
         "svo_aggregate": (None, [vp, i32, i32, i32, i32, i32, vp, i32]),
@@ -190,3 +193,44 @@ def lr_check(disp_l, disp_r, dir, max_diff=1, invalid=0xFFFF):
     H, W = dl.shape
     lib.svo_lr_check(_p(dl), _p(dr), W, H, dir, max_diff, invalid)
     return dl
+
+
+def step_offset(s, bx, by):
+    ox, oy = ct.c_int(0), ct.c_int(0)
+    lib.svo_step_offset(s, bx, by, ct.byref(ox), ct.byref(oy))
+    return ox.value, oy.value
+
+
+def cost2(cl, cr, D, dmin, sx, sy):
+    cl = _c(cl, np.uint64)
+    cr = _c(cr, np.uint64)
+    H, W = cl.shape
+    C = np.zeros((H, W, D), np.uint8)
+    lib.svo_cost2(_p(cl), _p(cr), W, H, D, dmin, sx, sy, _p(C))
+    return C
+
+
+def sgm2(left, right, D, dmin=0, sx=-1, sy=0, P1=10, P2=120, subpixel=True, threads=8):
+    """Mode S with a 2-D matching step (census -> cost2 -> 8 paths -> WTA)."""
+    cl, cr = census(left), census(right)
+    C = cost2(cl, cr, D, dmin, sx, sy)
+    S = aggregate(C, P1, P2, threads)
+    return wta(S, dmin, subpixel)
+
+
+def lr_check2(disp_l, disp_r, sx, sy, max_diff=1, invalid=0xFFFF):
+    dl = _c(disp_l, np.uint16).copy()
+    dr = _c(disp_r, np.uint16)
+    H, W = dl.shape
+    lib.svo_lr_check2(_p(dl), _p(dr), W, H, sx, sy, max_diff, invalid)
+    return dl
+
+
+def fuse_depth(disps, baselines, f, pixel_size, invalid=0xFFFF):
+    d = _c(disps, np.uint16)
+    N, H, W = d.shape
+    b = np.ascontiguousarray(baselines, dtype=np.float64)
+    out = np.zeros((H, W), np.float64)
+    nv = np.zeros((H, W), np.uint8)
+    lib.svo_fuse_depth(_p(d), N, W, H, _p(b), f, pixel_size, invalid, _p(out), _p(nv))
+    return out, nv

@@ -58,6 +58,32 @@ void svo_cost(const uint64_t* cl, const uint64_t* cr, int W, int H, int D, int d
             }
 }
 
+/* DESIGN.md §2.2 -- 2-D matching step. */
+void svo_step_offset(int s, int bx, int by, int* ox, int* oy) {
+    int ax = bx < 0 ? -bx : bx, ay = by < 0 ? -by : by;
+    int M = ax > ay ? ax : ay, m = ax > ay ? ay : ax;
+    int major = s, minor = (2 * s * m + M) / (2 * M);   /* round half up, s >= 0 */
+    int mx = ax >= ay ? major : minor, my = ax >= ay ? minor : major;
+    *ox = bx < 0 ? -mx : (bx > 0 ? mx : 0);
+    *oy = by < 0 ? -my : (by > 0 ? my : 0);
+}
+
+void svo_cost2(const uint64_t* cl, const uint64_t* cr, int W, int H, int D, int dmin, int sx,
+               int sy, uint8_t* C) {
+    for (int d = 0; d < D; d++) {
+        int ox, oy;
+        svo_step_offset(dmin + d, sx, sy, &ox, &oy);
+        for (int y = 0; y < H; y++)
+            for (int x = 0; x < W; x++) {
+                int xr = x + ox, yr = y + oy;
+                int c = 62;
+                if (xr >= 0 && xr < W && yr >= 0 && yr < H)
+                    c = popcount64(cl[(size_t)y * W + x] ^ cr[(size_t)yr * W + xr]);
+                C[((size_t)y * W + x) * D + d] = (uint8_t)c;
+            }
+    }
+}
+
 /* DESIGN.md §2.3 -- direction table r = 0..7 (step vectors p = q + r). */
 void svo_direction(int r, int* rx, int* ry) {
     static const int T[8][2] = {{1, 0}, {-1, 0}, {0, 1}, {0, -1},
@@ -228,4 +254,43 @@ void svo_lr_check(uint16_t* disp_l, const uint16_t* disp_r, int W, int H, int di
             if (diff < 0) diff = -diff;
             if (dr == invalid || diff > max_diff) *dl = invalid;
         }
+}
+
+void svo_lr_check2(uint16_t* disp_l, const uint16_t* disp_r, int W, int H, int sx, int sy,
+                   int max_diff, uint16_t invalid) {
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            uint16_t* dl = disp_l + (size_t)y * W + x;
+            if (*dl == invalid) continue;
+            int ox, oy;
+            svo_step_offset((int)*dl, sx, sy, &ox, &oy);
+            int xr = x + ox, yr = y + oy;
+            if (xr < 0 || xr >= W || yr < 0 || yr >= H) { *dl = invalid; continue; }
+            int dr = disp_r[(size_t)yr * W + xr];
+            int diff = (int)*dl - dr;
+            if (diff < 0) diff = -diff;
+            if (dr == invalid || diff > max_diff) *dl = invalid;
+        }
+}
+
+/* DESIGN.md §2.6 -- median depth over the valid maps (insertion sort). */
+void svo_fuse_depth(const uint16_t* disps, int n_maps, int W, int H, const double* baseline,
+                    double f, double pixel_size, uint16_t invalid, double* depth,
+                    uint8_t* n_valid) {
+    double v[64];
+    for (size_t p = 0; p < (size_t)W * H; p++) {
+        int n = 0;
+        for (int i = 0; i < n_maps && i < 64; i++) {
+            uint16_t d = disps[(size_t)i * W * H + p];
+            if (d == invalid || d == 0) continue;
+            double z = (baseline[i] * f) / ((double)d * pixel_size);
+            int j = n++;
+            while (j > 0 && v[j - 1] > z) { v[j] = v[j - 1]; j--; }
+            v[j] = z;
+        }
+        double out = 0.0;
+        if (n > 0) out = (n & 1) ? v[n / 2] : (v[n / 2 - 1] + v[n / 2]) * 0.5;
+        depth[p] = out;
+        if (n_valid) n_valid[p] = (uint8_t)n;
+    }
 }

@@ -93,6 +93,19 @@ void svo_census(const uint8_t* img, int W, int H, ptrdiff_t pitch, uint64_t* out
 void svo_cost(const uint64_t* cl, const uint64_t* cr, int W, int H, int D, int dmin, int dir,
               uint8_t* C);
 
+/* 2-D matching step.  (sx, sy) = integer baseline direction
+ * (bx, by), not both 0; with s = dmin + d the matched pixel is (x, y) +
+ * svo_step_offset(s, bx, by): s pixels along the major axis (|bx| >= |by|: x),
+ * round_half_up(s*m/M) along the minor one (m, M = minor/major |component|),
+ * each with the sign of its component.  Unit steps (+-1, 0), (0, +-1),
+ * (+-1, +-1) are the axis / 45-degree cases; by = 0 is svo_cost(dir = sign bx).
+ * Array pairs (parallel optical axes, equal f) have exactly this epipolar
+ * geometry; the rounding is the closed form of the reference's Bresenham
+ * (functions.cpp:299-321). */
+void svo_step_offset(int s, int bx, int by, int* ox, int* oy);
+void svo_cost2(const uint64_t* cl, const uint64_t* cr, int W, int H, int D, int dmin, int sx,
+               int sy, uint8_t* C);
+
 /* One SGM path direction: step vector (rx, ry); L u8 volume. */
 void svo_path(const uint8_t* C, int W, int H, int D, int rx, int ry, int P1, int P2, uint8_t* L);
 
@@ -115,6 +128,18 @@ void svo_sgm(const uint8_t* left, const uint8_t* right, int W, int H, ptrdiff_t 
  * |dL - dR(matched)| > max_diff are set to invalid. */
 void svo_lr_check(uint16_t* disp_l, const uint16_t* disp_r, int W, int H, int dir,
                   int max_diff, uint16_t invalid);
+/* 2-D form: the right-reference map was computed with (-sx, -sy); the left
+ * disparity d is followed to (x, y) + svo_step_offset(d, sx, sy). */
+void svo_lr_check2(uint16_t* disp_l, const uint16_t* disp_r, int W, int H, int sx, int sy,
+                   int max_diff, uint16_t invalid);
+
+/* Multi-pair depth fusion: per pixel, depth_i =
+ * (baseline_i * f) / ((double)disp_i * pixel_size) for every map i with
+ * disp_i != invalid and disp_i > 0; output the median (mean of the two middle
+ * values for an even count, f64), 0 where no map is valid.  n_valid nullable. */
+void svo_fuse_depth(const uint16_t* disps, int n_maps, int W, int H, const double* baseline,
+                    double f, double pixel_size, uint16_t invalid, double* depth,
+                    uint8_t* n_valid);
 
 #ifdef __cplusplus
 }

@@ -34,7 +34,7 @@ EXPORTED = [
     "sva_kernel_time", "sva_disparity_sgm", "sva_disparity_sgm_d", "sva_census_d",
     "sva_cost_d", "sva_paths_d", "sva_aggregate_d", "sva_wta_d", "sva_disparity_ref",
     "sva_disparity_ref_d", "sva_ref_endpoints_d", "sva_disparity_to_depth_d",
-    "sva_disparity_to_depth",
+    "sva_disparity_to_depth", "sva_fuse_depth_d", "sva_fuse_depth",
     "sva_batch_sgm",
 ]
 
@@ -45,7 +45,7 @@ class SgmParams(ct.Structure):
         ("D", ct.c_int32), ("dmin", ct.c_int32), ("dir", ct.c_int32),
         ("P1", ct.c_int32), ("P2", ct.c_int32), ("subpixel", ct.c_int32),
         ("lr_check", ct.c_int32), ("lr_max_diff", ct.c_int32),
-        ("invalid", ct.c_uint16), ("_pad", ct.c_uint16),
+        ("invalid", ct.c_uint16), ("_pad", ct.c_uint16), ("dir_y", ct.c_int32),
     ]
 
 
@@ -128,6 +128,8 @@ def _load() -> ct.CDLL:
         "sva_ref_endpoints_d": (i32, [vp, i32, i32, P(Camera), P(Camera), i32, dbl, dbl, vp, vp]),
         "sva_disparity_to_depth_d": (i32, [vp, vp, i32, dbl, dbl, dbl, vp]),
         "sva_disparity_to_depth": (i32, [vp, vp, i32, dbl, dbl, dbl, vp]),
+        "sva_fuse_depth_d": (i32, [vp, vp, i32, i32, i32, P(dbl), dbl, dbl, ct.c_uint16, vp, vp]),
+        "sva_fuse_depth": (i32, [vp, vp, i32, i32, i32, P(dbl), dbl, dbl, ct.c_uint16, vp, vp]),
         "sva_batch_sgm": (i32, [P(vp), i32, P(PairJob), i32, P(SgmParams)]),
     }
     for name, (res, args) in sig.items():
@@ -278,6 +280,22 @@ class Context:
     def ref_endpoints_d(self, W, H, cref, coth, k, t_near, t_far, ends, valid):
         self._chk(lib.sva_ref_endpoints_d(self.h, W, H, ct.byref(cref), ct.byref(coth), k,
                                           t_near, t_far, _ptr(ends), _ptr(valid)))
+
+    def fuse_depth(self, disps: np.ndarray, baselines, f, pixel_size, invalid=0xFFFF):
+        d = np.ascontiguousarray(disps, dtype=np.uint16)
+        N, H, W = d.shape
+        b = (ct.c_double * N)(*[float(v) for v in baselines])
+        out = np.zeros((H, W), np.float64)
+        nv = np.zeros((H, W), np.uint8)
+        self._chk(lib.sva_fuse_depth(self.h, _ptr(d), N, W, H, b, f, pixel_size, invalid,
+                                     _ptr(out), _ptr(nv)))
+        return out, nv
+
+    def fuse_depth_d(self, disps, n_maps, W, H, baselines, f, pixel_size, invalid, depth,
+                     n_valid=None):
+        b = (ct.c_double * n_maps)(*[float(v) for v in baselines])
+        self._chk(lib.sva_fuse_depth_d(self.h, _ptr(disps), n_maps, W, H, b, f, pixel_size,
+                                       invalid, _ptr(depth), _ptr(n_valid)))
 
     def disparity_to_depth(self, disp: np.ndarray, cam_distance, f, pixel_size):
         d = np.ascontiguousarray(disp, dtype=np.uint8)

@@ -139,8 +139,12 @@ int check_sgm(Ctx* c, const sva_sgm_params* p, int W) {
     if (p->D <= 0) return fail(c, SVA_ERR_INVALID_ARG, "D must be positive");
     if (!paths_supported(p->D))
         return fail(c, SVA_ERR_UNSUPPORTED, "GPU path built for D in {64,128,192,256}");
-    if (p->dir != 1 && p->dir != -1) return fail(c, SVA_ERR_INVALID_ARG, "dir must be +1 or -1");
+    if (p->dir < -255 || p->dir > 255 || p->dir_y < -255 || p->dir_y > 255 ||
+        (p->dir == 0 && p->dir_y == 0))
+        return fail(c, SVA_ERR_INVALID_ARG, "(dir, dir_y) must be a nonzero step, |comp| <= 255");
     if (p->dmin < 0) return fail(c, SVA_ERR_INVALID_ARG, "dmin must be >= 0");
+    if (p->dmin + p->D > 65535)
+        return fail(c, SVA_ERR_INVALID_ARG, "dmin + D must fit the u16 disparity map");
     if (p->P1 < 0 || p->P2 < 0 || p->P1 > 193 || p->P2 > 193)
         return fail(c, SVA_ERR_INVALID_ARG, "penalties must satisfy 0 <= P1, P2 <= 193");
     if (p->lr_check && p->lr_max_diff < 0)
@@ -162,17 +166,19 @@ int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int
     uint8_t* C = (uint8_t*)c->cost.ptr;
     uint8_t* L8 = (uint8_t*)c->paths.ptr;
     SVA_HIP(c, launch_census_pair(*c, left, right, W, H, pitch, cl, cr), "census launch");
-    SVA_HIP(c, launch_cost(*c, cl, cr, W, H, p->D, p->dmin, p->dir, C), "cost launch");
+    SVA_HIP(c, launch_cost2(*c, cl, cr, W, H, p->D, p->dmin, p->dir, p->dir_y, C), "cost launch");
     SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
     SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, disp, sub), "wta launch");
     if (p->lr_check) {
         SVA_HIP(c, c->disp_r.ensure(np * 2), "lr workspace");
         uint16_t* dr = (uint16_t*)c->disp_r.ptr;
-        // right image as reference: roles of the census maps swap, dir flips
-        SVA_HIP(c, launch_cost(*c, cr, cl, W, H, p->D, p->dmin, -p->dir, C), "cost launch");
+        // right image as reference: roles of the census maps swap, the step flips
+        SVA_HIP(c, launch_cost2(*c, cr, cl, W, H, p->D, p->dmin, -p->dir, -p->dir_y, C),
+                "cost launch");
         SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
         SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, dr, nullptr), "wta launch");
-        SVA_HIP(c, launch_lr_check(*c, disp, dr, W, H, p->dir, p->lr_max_diff, p->invalid),
+        SVA_HIP(c, launch_lr_check(*c, disp, dr, W, H, p->dir, p->dir_y, p->lr_max_diff,
+                                   p->invalid),
                 "lr launch");
     }
     return SVA_OK;
@@ -405,7 +411,7 @@ int sva_cost_d(void* ctx, const uint64_t* cl, const uint64_t* cr, int W, int H,
     int s;
     if ((s = check_sgm(c, p, W))) return s;
     if (!cl || !cr || !C || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
-    SVA_HIP(c, launch_cost(*c, cl, cr, W, H, p->D, p->dmin, p->dir, C), "cost launch");
+    SVA_HIP(c, launch_cost2(*c, cl, cr, W, H, p->D, p->dmin, p->dir, p->dir_y, C), "cost launch");
     return SVA_OK;
 }
 
@@ -540,6 +546,55 @@ int sva_disparity_to_depth(void* ctx, const uint8_t* disp, int n, double cam_dis
                                     (double*)c->out_a.ptr), "depth launch");
     SVA_HIP(c, hipMemcpyAsync(depth, c->out_a.ptr, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream),
             "download");
+    SVA_HIP(c, hipStreamSynchronize(c->stream), "sync");
+    return SVA_OK;
+}
+
+int check_fuse(Ctx* c, const uint16_t* disps, int n_maps, int W, int H, const double* b,
+               const double* depth) {
+    if (!disps || !b || !depth) return fail(c, SVA_ERR_INVALID_ARG, "null pointer");
+    if (n_maps < 1 || n_maps > 32) return fail(c, SVA_ERR_UNSUPPORTED, "n_maps must be 1..32");
+    if (W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "image size must be positive");
+    return SVA_OK;
+}
+
+int sva_fuse_depth_d(void* ctx, const uint16_t* disps, int n_maps, int W, int H,
+                     const double* baselines, double f, double pixel_size, uint16_t invalid,
+                     double* depth, uint8_t* n_valid) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_fuse(c, disps, n_maps, W, H, baselines, depth))) return s;
+    double num[32];
+    for (int i = 0; i < n_maps; i++) num[i] = baselines[i] * f;
+    SVA_HIP(c, launch_fuse_depth(*c, disps, n_maps, (size_t)W * H, num, pixel_size, invalid,
+                                 depth, n_valid), "fuse launch");
+    return SVA_OK;
+}
+
+int sva_fuse_depth(void* ctx, const uint16_t* disps, int n_maps, int W, int H,
+                   const double* baselines, double f, double pixel_size, uint16_t invalid,
+                   double* depth, uint8_t* n_valid) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_fuse(c, disps, n_maps, W, H, baselines, depth))) return s;
+    const size_t np = (size_t)W * H, in_bytes = np * 2 * (size_t)n_maps;
+    double num[32];
+    for (int i = 0; i < n_maps; i++) num[i] = baselines[i] * f;
+    SVA_HIP(c, c->in_a.ensure(in_bytes), "staging");
+    SVA_HIP(c, c->out_a.ensure(np * 8), "staging");
+    SVA_HIP(c, c->out_b.ensure(np), "staging");
+    SVA_HIP(c, hipMemcpyAsync(c->in_a.ptr, disps, in_bytes, hipMemcpyHostToDevice, c->stream),
+            "upload");
+    SVA_HIP(c, launch_fuse_depth(*c, (const uint16_t*)c->in_a.ptr, n_maps, np, num, pixel_size,
+                                 invalid, (double*)c->out_a.ptr, (uint8_t*)c->out_b.ptr),
+            "fuse launch");
+    SVA_HIP(c, hipMemcpyAsync(depth, c->out_a.ptr, np * 8, hipMemcpyDeviceToHost, c->stream),
+            "download");
+    if (n_valid)
+        SVA_HIP(c, hipMemcpyAsync(n_valid, c->out_b.ptr, np, hipMemcpyDeviceToHost, c->stream),
+                "download");
     SVA_HIP(c, hipStreamSynchronize(c->stream), "sync");
     return SVA_OK;
 }

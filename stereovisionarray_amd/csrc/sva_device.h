@@ -62,4 +62,16 @@ __device__ __forceinline__ unsigned pack4(unsigned p01, unsigned p23) {
     return __builtin_amdgcn_perm(p23, p01, 0x06040200u);
 }
 
+// Matched-pixel offset for match distance s >= 0 along the integer baseline
+// direction (bx, by): s pixels along the major axis,
+// round_half_up(s*m/M) along the minor one, each with its component's sign.
+// Same integer expression as oracle svo_step_offset.
+__device__ __forceinline__ int2 step_offset(int s, int bx, int by) {
+    const int ax = bx < 0 ? -bx : bx, ay = by < 0 ? -by : by;
+    const int M = ax > ay ? ax : ay, m = ax > ay ? ay : ax;
+    const int minor = (m == 0) ? 0 : (m == M ? s : (2 * s * m + M) / (2 * M));
+    const int mx = ax >= ay ? s : minor, my = ax >= ay ? minor : s;
+    return make_int2(bx < 0 ? -mx : (bx > 0 ? mx : 0), by < 0 ? -my : (by > 0 ? my : 0));
+}
+
 }  // namespace sva

@@ -93,7 +93,15 @@ hipError_t launch_wta_from_paths(Ctx& c, const uint8_t* L8, int W, int H, int D,
 hipError_t launch_wta_from_sum(Ctx& c, const uint16_t* S, int W, int H, int D, int dmin,
                                uint16_t* disp, float* sub);
 hipError_t launch_lr_check(Ctx& c, uint16_t* disp_l, const uint16_t* disp_r, int W, int H,
-                           int dir, int max_diff, uint16_t invalid);
+                           int sx, int sy, int max_diff, uint16_t invalid);
+// 2-D matching step (sy != 0); sy == 0 forwards to launch_cost(dir = sx).
+hipError_t launch_cost2(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,
+                        int dmin, int sx, int sy, uint8_t* C);
+// Median depth fusion over n_maps <= 32 u16 maps.
+// num[i] = baseline_i * f (host-computed, same f64 product as the oracle).
+hipError_t launch_fuse_depth(Ctx& c, const uint16_t* disps, int n_maps, size_t np,
+                             const double* num, double pixel_size, uint16_t invalid,
+                             double* depth, uint8_t* n_valid);
 // refpath.hip
 hipError_t launch_ref_endpoints(Ctx& c, int W, int H, const sva_camera& cref,
                                 const sva_camera& coth, int k, double t_near, double t_far,

@@ -243,3 +243,63 @@ def test_lr_check_kat(oracle):
     assert out[0].tolist() == [0, 0xFFFF, 0xFFFF, 0xFFFF]
     out = oracle.lr_check(dl, dr, dir=-1, max_diff=2, invalid=0xFFFF)
     assert out[0].tolist() == [0, 0xFFFF, 2, 1]
+
+
+def test_cost2_kat(oracle):
+    """2-D step: hand-placed census words."""
+    cl = np.zeros((4, 3), np.uint64)
+    cr = np.zeros((4, 3), np.uint64)
+    cl[1, 1] = 0b1011
+    cr[1, 1], cr[2, 1], cr[3, 2], cr[0, 1] = 0b0001, 0b1000, 0b1011, 0b1111
+    C = oracle.cost2(cl, cr, D=3, dmin=0, sx=0, sy=1)     # (1,1) -> (1,1),(1,2),(1,3)
+    assert C[1, 1].tolist() == [2, 2, 3]
+    C = oracle.cost2(cl, cr, D=3, dmin=0, sx=1, sy=1)     # (1,1),(2,2),(3,3)->outside
+    assert C[1, 1].tolist() == [2, 3, 62]
+    C = oracle.cost2(cl, cr, D=3, dmin=1, sx=0, sy=-1)    # (1,0), then outside
+    assert C[1, 1].tolist() == [1, 62, 62]
+    # sy = 0 is exactly the 1-D cost
+    rng = np.random.default_rng(0)
+    a = rng.integers(0, 1 << 62, size=(5, 40), dtype=np.int64).astype(np.uint64)
+    b = rng.integers(0, 1 << 62, size=(5, 40), dtype=np.int64).astype(np.uint64)
+    for dr in (-1, 1):
+        assert np.array_equal(oracle.cost2(a, b, 16, 2, dr, 0), oracle.cost(a, b, 16, 2, dr))
+
+
+def test_lr_check2_kat(oracle):
+    dl = np.array([[0], [1], [1], [2]], np.uint16)
+    dr = np.array([[5], [0], [1], [9]], np.uint16)
+    # sy=-1: (x, y) -> (x, y - d); y=1 d=1 -> dr[0]=5 reject; y=2 d=1 -> dr[1]=0 ok (|1-0|<=1)
+    # y=3 d=2 -> dr[1]=0 reject (2 > 1); y=0 d=0 -> dr[0]=5 reject
+    out = oracle.lr_check2(dl, dr, 0, -1, 1, 0xFFFF)
+    assert out[:, 0].tolist() == [0xFFFF, 0xFFFF, 1, 0xFFFF]
+    out = oracle.lr_check2(dl, dr, 0, 1, 1, 0xFFFF)       # y=3 d=2 -> row 5: outside
+    assert out[3, 0] == 0xFFFF
+
+
+def test_fuse_depth_kat(oracle):
+    """DESIGN.md §2.6 by hand: b*f/(d*ps), median, mean of the middle two."""
+    f, ps = 0.05, 1e-4
+    d = np.array([[[10, 0xFFFF]], [[20, 5]], [[0, 0]]], np.uint16)    # 3 maps, 1x2
+    z, n = oracle.fuse_depth(d, [0.05, 0.05, 0.1], f, ps)
+    # pixel 0: 2.5 and 1.25 (map 2 has d=0: skipped) -> mean 1.875
+    # pixel 1: map 1 only -> 0.0025 / 5e-4 = 5
+    assert z[0].tolist() == pytest.approx([1.875, 5.0], rel=1e-14) and n[0].tolist() == [2, 1]
+    d = np.array([[[4]], [[8]], [[2]], [[0xFFFF]]], np.uint16)
+    z, n = oracle.fuse_depth(d, [0.1, 0.1, 0.1, 0.1], 1.0, 1.0)     # 0.025, 0.0125, 0.05
+    assert z[0, 0] == pytest.approx(0.025, rel=1e-14) and n[0, 0] == 3
+    z, n = oracle.fuse_depth(np.full((2, 1, 1), 0xFFFF, np.uint16), [1, 1], 1.0, 1.0)
+    assert z[0, 0] == 0.0 and n[0, 0] == 0
+
+
+def test_step_offset_kat(oracle):
+    """DESIGN.md §2.2 offsets by hand; and the synth restatement agrees."""
+    assert [oracle.step_offset(s, 2, 1) for s in range(6)] == \
+        [(0, 0), (1, 1), (2, 1), (3, 2), (4, 2), (5, 3)]       # round(s/2), half up
+    assert [oracle.step_offset(s, -1, 3) for s in range(5)] == \
+        [(0, 0), (0, 1), (-1, 2), (-1, 3), (-1, 4)]            # round(s/3)
+    assert oracle.step_offset(7, 0, -1) == (0, -7)
+    assert oracle.step_offset(7, -1, -1) == (-7, -7)
+    assert oracle.step_offset(7, 5, 0) == (7, 0)
+    for bx, by in [(2, 1), (-3, -2), (1, -4), (0, 2), (7, 7)]:
+        for s in range(0, 300, 7):
+            assert oracle.step_offset(s, bx, by) == tuple(int(v) for v in synth.step_offset(s, bx, by))

@@ -20,6 +20,8 @@ for step in "$@"; do
     pytest_all) run pytest_gpu_all 1500 python -m pytest tests -q -m gpu ;;
     pytest_slow) run pytest_gpu_slow 900 python -m pytest tests -q -m "gpu and slow" ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    pytest_array) run pytest_array 900 python -m pytest tests/test_array_gpu.py -q -m gpu ;;
+    array) run array 600 python bench.py --workload array8 --steps 5 --warmup 2 --no-cpu-baseline ;;
     bench4k) run bench4k 600 python bench.py --steps 5 --warmup 2 --workload 4k_d256 --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
