@@ -225,7 +225,7 @@ def run_array(a, wl, world, rank, local, dev):
         edge = np.zeros(W, bool)
         cuts = np.flatnonzero(np.diff(delta[0]) != 0)
         for c in cuts:
-            edge[max(0, c - D): c + D] = True
+            edge[max(0, c - 48): c + 48] = True
         inner = np.zeros((H, W), bool)
         inner[D:H - D, D:W - D] = True
         inner &= ~edge[None, :]

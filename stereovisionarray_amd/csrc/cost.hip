@@ -67,62 +67,77 @@ __global__ __launch_bounds__(BLOCK) void hamming_cost_kernel(const uint64_t* __r
 }
 
 // 2-D matching step: the word for (x, y, d) sits at
-// (x, y) + step_offset(s, bx, by), s = dmin + d, by != 0 (vertical, diagonal
-// and any other integer baseline direction of an array pair).  The per-block
-// offset table (one division per disparity) lives in LDS.  Consecutive disparities now walk down rows, so no word is shared
-// between the D disparities of one pixel; what a row of pixels shares is the
-// word at the same s: the PX pixels of a block read, per s, PX consecutive
-// words of one census row.  The block stages that D x PX tile in LDS once
-// (coalesced row segments) and every thread then reads its 16 words from LDS.
-// LDS slot of (s-index e, pixel p): e*PX + (p + G*(e>>4)) % PX.  The 32 lanes of
-// a half-wave are 32/NC pixels x NC chunks; rotating each chunk's row by G =
-// 32/NC words puts the 32 lanes' reads in 32 distinct bank pairs (D=64, 128;
-// D=192/256 keep a 2-way conflict, the rows are narrower than a bank sweep).
-// Out-of-image words are staged as a word with bit 63 set, which no census
-// word has (bits 0..61), and read back as cost 62.
+// q + off(s), off = step_offset(., bx, by), s = dmin + d, by != 0 (vertical,
+// diagonal and any other integer baseline direction of an array pair).
+//
+// Reuse along the lattice step v = (bx, by): rounding commutes with adding an
+// integer, so off(s + r*M) = off(s) + r*v (M = max(|bx|, |by|)) and pixel
+// q + r*v at distance s reads the word that q reads at distance s + r*M.  A
+// workgroup therefore owns PX base pixels b of one row y0 and the R pixels
+// b + r*v (r < R) above each: a sheared PX x R tile.  It needs, per base pixel,
+// only the words q_b + off(dmin + t) for t < T = D + M*(R-1) -- staged once in
+// LDS as coalesced row segments (about T/R ~ 5 words per pixel at D=128 instead
+// of D) -- then writes R rows of PX*D contiguous cost bytes.
+// Tiling: rows y0 + r*by of band/phase (|by| interleaved phases per band of
+// R*|by| rows; by < 0 bands run up from the bottom); base columns over
+// [bmin, bmin + ncolb*PX) so the sheared rows cover [0, W); pixels outside the
+// image are skipped.
+// LDS slot of (t, b): t*PX + (b + G*(t>>4)) % PX.  A half-wave is 32/NC pixels
+// x NC chunks reading t = 16c + j (same j): t>>4 = c + (j>>4), so rotating by
+// G = 32/NC words per 16 t puts the 32 lanes on 32 distinct bank pairs (D=64,
+// 128; D=192/256 keep a 2-way conflict).  Out-of-image words are staged with
+// bit 63 set, which no census word has (bits 0..61), and read back as 62.
 constexpr uint64_t kOutside = 1ull << 63;
+constexpr int kCost2LdsBytes = 64 * 1024;
 
 template <int NC>
-__global__ __launch_bounds__(BLOCK) void hamming_cost2_kernel(const uint64_t* __restrict__ cl,
-                                                               const uint64_t* __restrict__ cr,
-                                                               int W, int H, int dmin, int bx,
-                                                               int by, uint8_t* __restrict__ C) {
+__global__ __launch_bounds__(BLOCK) void hamming_cost2_kernel(
+    const uint64_t* __restrict__ cl, const uint64_t* __restrict__ cr, int W, int H, int dmin,
+    int bx, int by, int R, int T, int ncolb, int bmin, uint8_t* __restrict__ C) {
     constexpr int D = NC * 16, PX = BLOCK / NC, G = 32 / NC > 0 ? 32 / NC : 1;
-    __shared__ uint64_t rw[D * PX];
-    __shared__ int2 off[D];
-    const int blocks_per_row = (W + PX - 1) / PX;
-    const int y = blockIdx.x / blocks_per_row;
-    const int x0 = (blockIdx.x - y * blocks_per_row) * PX;
-    for (int e = threadIdx.x; e < D; e += BLOCK) off[e] = step_offset(dmin + e, bx, by);
+    extern __shared__ uint64_t smem[];
+    uint64_t* rw = smem;                       // [T][PX] census words
+    int2* off = reinterpret_cast<int2*>(smem + (size_t)T * PX);
+    const int aby = by < 0 ? -by : by, abx = bx < 0 ? -bx : bx;
+    const int M = abx > aby ? abx : aby;
+    const int colb = blockIdx.x % ncolb, rb = blockIdx.x / ncolb;
+    const int band = rb / aby, phase = rb - band * aby;
+    const int y0 = by > 0 ? band * R * aby + phase : (H - 1) - (band * R * aby + phase);
+    const int X0 = bmin + colb * PX;
+    for (int t = threadIdx.x; t < T; t += BLOCK) off[t] = step_offset(dmin + t, bx, by);
     __syncthreads();
-    for (int i = threadIdx.x; i < D * PX; i += BLOCK) {
-        const int e = i / PX, p = i - e * PX;
-        const int2 o = off[e];
-        const int xr = x0 + p + o.x, yr = y + o.y;
+    for (int i = threadIdx.x; i < T * PX; i += BLOCK) {
+        const int t = i / PX, b = i - t * PX;
+        const int2 o = off[t];
+        const int xr = X0 + b + o.x, yr = y0 + o.y;
         uint64_t w = kOutside;
         if ((unsigned)xr < (unsigned)W && (unsigned)yr < (unsigned)H) w = cr[(size_t)yr * W + xr];
-        rw[e * PX + (p + G * (e >> 4)) % PX] = w;
+        rw[t * PX + (b + G * (t >> 4)) % PX] = w;
     }
     __syncthreads();
     const int lp = threadIdx.x / NC;
-    const int x = x0 + lp;
-    if (lp >= PX || x >= W) return;  // D=192: 256 % 12 != 0 leaves idle lanes
+    if (lp >= PX) return;  // D=192: 256 % 12 != 0 leaves idle lanes
     const int c = threadIdx.x - lp * NC;
-    const uint64_t l = cl[(size_t)y * W + x];
-    const uint64_t* col = rw + (c * 16) * PX + (lp + G * c) % PX;
-    unsigned out[4];
+    for (int r = 0; r < R; r++) {
+        const int x = X0 + lp + r * bx, y = y0 + r * by;
+        if ((unsigned)x >= (unsigned)W || (unsigned)y >= (unsigned)H) continue;
+        const uint64_t l = cl[(size_t)y * W + x];
+        const int j0 = r * M;                 // t = 16c + j0 + k
+        unsigned out[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        unsigned w = 0;
+        for (int q = 0; q < 4; q++) {
+            unsigned w = 0;
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const uint64_t v = l ^ col[(q * 4 + b) * PX];
-            const unsigned cst = (v >> 63) ? 62u : (unsigned)__popcll(v);
-            w |= cst << (8 * b);
+            for (int b = 0; b < 4; b++) {
+                const int j = j0 + q * 4 + b, t = c * 16 + j;
+                const uint64_t v = l ^ rw[t * PX + (lp + G * c + G * (j >> 4)) % PX];
+                const unsigned cst = (v >> 63) ? 62u : (unsigned)__popcll(v);
+                w |= cst << (8 * b);
+            }
+            out[q] = w;
         }
-        out[q] = w;
+        *(uint4*)(C + ((size_t)y * W + x) * D + c * 16) = make_uint4(out[0], out[1], out[2], out[3]);
     }
-    *(uint4*)(C + ((size_t)y * W + x) * D + c * 16) = make_uint4(out[0], out[1], out[2], out[3]);
 }
 
 }  // namespace
@@ -131,15 +146,34 @@ hipError_t launch_cost2(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, i
                         int dmin, int sx, int sy, uint8_t* C) {
     if (sy == 0) return launch_cost(c, cl, cr, W, H, D, dmin, sx > 0 ? 1 : -1, C);
     ScopedKernelTimer t(c, "cost");
+    // reduce the step to its primitive lattice vector (same offsets, more reuse)
+    int a = sx < 0 ? -sx : sx, b = sy < 0 ? -sy : sy;
+    while (b) { int r = a % b; a = b; b = r; }
+    const int bx = sx / a, by = sy / a;
+    const int abx = bx < 0 ? -bx : bx, aby = by < 0 ? -by : by, M = abx > aby ? abx : aby;
     const int nc = D / 16, px = BLOCK / nc;
-    const dim3 grid(((W + px - 1) / px) * H);
+    const int tmax = kCost2LdsBytes / (8 * (px + 1));
+    int R = 1 + (tmax - D) / M;
+    if (R > 32) R = 32;
+    if (R < 1) return hipErrorInvalidValue;
+    const int T = D + M * (R - 1);
+    const int span = (R - 1) * abx;
+    const int bmin = bx > 0 ? -span : 0;
+    const int ncolb = (W + span + px - 1) / px;
+    const int nbands = (H + R * aby - 1) / (R * aby);
+    const dim3 grid((unsigned)(ncolb * nbands * aby));
+    const size_t lds = (size_t)T * px * 8 + (size_t)T * 8;
+#define SVA_COST2(NC)                                                                          \
+    hipLaunchKernelGGL(hamming_cost2_kernel<NC>, grid, dim3(BLOCK), lds, c.stream, cl, cr, W, H, \
+                       dmin, bx, by, R, T, ncolb, bmin, C)
     switch (nc) {
-        case 4: hipLaunchKernelGGL(hamming_cost2_kernel<4>, grid, dim3(BLOCK), 0, c.stream, cl, cr, W, H, dmin, sx, sy, C); break;
-        case 8: hipLaunchKernelGGL(hamming_cost2_kernel<8>, grid, dim3(BLOCK), 0, c.stream, cl, cr, W, H, dmin, sx, sy, C); break;
-        case 12: hipLaunchKernelGGL(hamming_cost2_kernel<12>, grid, dim3(BLOCK), 0, c.stream, cl, cr, W, H, dmin, sx, sy, C); break;
-        case 16: hipLaunchKernelGGL(hamming_cost2_kernel<16>, grid, dim3(BLOCK), 0, c.stream, cl, cr, W, H, dmin, sx, sy, C); break;
+        case 4: SVA_COST2(4); break;
+        case 8: SVA_COST2(8); break;
+        case 12: SVA_COST2(12); break;
+        case 16: SVA_COST2(16); break;
         default: return hipErrorInvalidValue;
     }
+#undef SVA_COST2
     return hipGetLastError();
 }
 

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 SUB_TOL = 1e-5
 STEPS_2D = [(0, -1), (0, 1), (-1, -1), (1, 1), (1, -1), (-1, 1), (2, -1), (-1, 3), (-3, -2),
-            (2, 0)]
+            (2, 0), (2, 2), (-4, 2)]
 
 
 def dev(a, d):
@@ -64,6 +64,20 @@ def test_full_pipeline_2d(ctx, sva, oracle, W, H, D, dmin, sx, sy):
     od, osub = oracle.sgm2(L, R, D, dmin, sx, sy, subpixel=True)
     assert np.array_equal(disp, od)
     assert np.max(np.abs(sub - osub)) <= SUB_TOL
+
+
+@pytest.mark.parametrize("sx,sy", [(0, -1), (-1, -1), (2, 1), (-1, 3)])
+def test_cost2_large(ctx, sva, oracle, torch_dev, sx, sy):
+    """Many sheared tiles / bands and a large dmin (offset table > D)."""
+    W, H, D, dmin = 333, 517, 128, 40
+    L, R, _ = synth.stereo_pair2(H, W, D, dmin, sx, sy, seed=7)
+    cl, cr = oracle.census(L), oracle.census(R)
+    C = torch.zeros((H, W, D), dtype=torch.uint8, device=torch_dev)
+    p = sva.default_params(D=D, dmin=dmin, dir=sx, dir_y=sy)
+    d_cl, d_cr = dev(cl.view(np.int64), torch_dev), dev(cr.view(np.int64), torch_dev)
+    ctx.cost_d(d_cl.data_ptr(), d_cr.data_ptr(), W, H, p, C.data_ptr())
+    run_sync(ctx)
+    assert np.array_equal(host(C), oracle.cost2(cl, cr, D, dmin, sx, sy))
 
 
 def test_vertical_shift_exact(ctx, sva):
