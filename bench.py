@@ -36,9 +36,16 @@ WORKLOADS = {
     "1080p_d192": dict(W=1920, H=1080, D=192),   # BASELINE configs[4] per-pair shape
     "vga_d64": dict(W=640, H=480, D=64),         # BASELINE configs[0] shape
     "1080half_d128": dict(W=1920, H=540, D=128), # experiment: C fits the Infinity Cache
-    # BASELINE configs[3]: 8-camera array (2x4 grid), all 28 pairwise baselines,
-    # pairs sharded over ranks, gather + per-reference-camera median fusion
-    "array8": dict(W=1920, H=1080, D=128, array=(2, 4)),
+    # BASELINE configs[3] as SURVEY.md §8d spells it: getCameraPairs(TO_CENTER_SMALL)
+    # = 12 <-> {6,7,8,11,13,16,17,18} (functions.cpp:156-165), one pair per GPU at
+    # N=8, gather + median fusion around camera 12
+    "center8": dict(W=1920, H=1080, D=128, rig="center8"),
+    # BASELINE configs[3] wording: an 8-camera array (2x4 grid), all 28 pairwise
+    # baselines, fused per reference camera
+    "grid8_all": dict(W=1920, H=1080, D=128, rig="grid8_all"),
+    # BASELINE configs[4]: 256 synthetic 1080p pairs (seeds 0-255), D=192,
+    # sharded over the ranks (32 per GPU at N=8): fixed total, strong scaling
+    "batch256_d192": dict(W=1920, H=1080, D=192, total_pairs=256),
 }
 
 ARRAY_PITCH = 0.05             # m between grid neighbours (CameraStereoVision.cpp:34-39)
@@ -146,13 +153,25 @@ def roofline_of(kernels, W, H, D, workload):
             "alg_bytes_per_launch": alg_bytes}
 
 
+def rig_of(name):
+    """(grid positions, pairs, label).  Positions are in grid units relative to
+    the first pair's reference camera, which therefore sees the texture
+    unwarped (used by the sanity check)."""
+    from stereovisionarray_amd import synth
+    if name == "center8":
+        g = [(i % 5 - 2, i // 5 - 2) for i in range(25)]      # 5x5, camera 12 at (0,0)
+        return g, [(12, j) for j in (6, 7, 8, 11, 13, 16, 17, 18)], \
+            "getCameraPairs(TO_CENTER_SMALL): 12 <-> {6,7,8,11,13,16,17,18}"
+    g = synth.array_grid(2, 4)
+    return g, synth.array_pairs(len(g)), "2x4 grid, all 28 pairwise baselines"
+
+
 def run_array(a, wl, world, rank, local, dev):
-    """BASELINE configs[3]: an 8-camera array (2x4 grid), all 28 pairwise
-    baselines at 1080p D=128.  Pair u (grouped by reference camera) is matched
-    by rank u mod N along its own baseline step; the u16 maps
-    are gathered to rank 0 (RCCL), which fuses, per reference camera, the
-    median depth over that camera's pairs.  Total work is
-    fixed (strong scaling)."""
+    """BASELINE configs[3]: camera-array pairs at 1080p D=128.  Pair u
+    (grouped by reference camera) is matched by rank u mod N along its own
+    baseline step; the u16 maps are gathered to rank 0
+    (RCCL), which fuses, per reference camera, the median depth over that
+    camera's pairs.  Total work is fixed (strong scaling)."""
     import torch
     import torch.distributed as dist
     import stereovisionarray_amd as sva
@@ -160,14 +179,13 @@ def run_array(a, wl, world, rank, local, dev):
     from stereovisionarray_amd import synth
 
     W, H, D = wl["W"], wl["H"], wl["D"]
-    rows, cols = wl["array"]
-    grid = synth.array_grid(rows, cols)
-    pairs = synth.array_pairs(len(grid))
+    grid, pairs, rig_label = rig_of(wl["rig"])
     n_units = len(pairs)
     kmax = max(synth.pair_step(grid[i], grid[j])[2] for i, j in pairs)
-    dmax = (D - 1) // kmax
+    dmax = min((D - 1) // kmax, 100)
     delta = synth.array_delta(H, W, dmax)
-    views_np = synth.array_views(H, W, grid, delta, seed=7)
+    used = sorted({c for p in pairs for c in p})
+    views_np = dict(zip(used, synth.array_views(H, W, [grid[c] for c in used], delta, seed=7)))
 
     ctx = sva.Context(local)
     stream = torch.cuda.Stream(dev)
@@ -185,12 +203,11 @@ def run_array(a, wl, world, rank, local, dev):
     disp = torch.zeros((len(mine), H, W), dtype=torch.int16, device=dev)
     # fusion groups on rank 0: reference camera i owns pairs [off, off + n)
     groups, off = [], 0
-    for i in range(len(grid)):
+    for i in dict.fromkeys(p[0] for p in pairs):     # pairs are grouped by reference
         n = sum(1 for p in pairs if p[0] == i)
-        if n:
-            bases = [synth.pair_step(grid[i], grid[j])[2] * ARRAY_PITCH
-                     for (ii, j) in pairs[off:off + n]]
-            groups.append((i, off, n, bases))
+        bases = [synth.pair_step(grid[i], grid[j])[2] * ARRAY_PITCH
+                 for (_, j) in pairs[off:off + n]]
+        groups.append((i, off, n, bases))
         off += n
     depth = torch.zeros((len(groups), H, W), dtype=torch.float64, device=dev)
     nvalid = torch.zeros((len(groups), H, W), dtype=torch.uint8, device=dev)
@@ -231,8 +248,8 @@ def run_array(a, wl, world, rank, local, dev):
         inner &= ~edge[None, :]
         exact = float(np.mean(np.abs(z0[inner] - truth[inner]) <= 1e-9 * truth[inner]))
         out = {
-            "metric": "Mdisparities/sec (W·H·D/s), 8-camera array, all 28 pairwise "
-                      "baselines, 1080p D=128, gather + fuse",
+            "metric": f"Mdisparities/sec (W·H·D/s), camera array ({rig_label}), "
+                      f"{W}x{H} D={D}, gather + fuse",
             "value": round(value, 1),
             "unit": "Mdisp/s",
             "n_gpus": world,
@@ -243,16 +260,16 @@ def run_array(a, wl, world, rank, local, dev):
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u16",
-            "data": "synthetic 2x4 array views of one MT19937 texture warped by 12 "
+            "data": "synthetic array views of one MT19937 texture warped by 12 "
                     f"stripe planes (per-grid-unit disparity 4..{dmax} px)",
-            "config": {"workload": f"array8: 2x4 grid, {n_units} pairs {W}x{H} D={D} Mode S "
-                                   "along each pair's baseline step, RCCL gather, per-camera "
-                                   "median fusion on rank 0",
+            "config": {"workload": f"{a.workload}: {rig_label}, {n_units} pairs {W}x{H} D={D} "
+                                   "Mode S along each pair's baseline step, RCCL gather, "
+                                   "per-camera median fusion on rank 0",
                        "W": W, "H": H, "D": D, "P1": 10, "P2": 120, "pairs": n_units,
                        "parallelism": f"pairs sharded over {world} rank(s), gather to rank 0"},
             "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
             "fused_maps_per_s": round(len(groups) * a.steps / elapsed, 2),
-            "cam0_interior_depth_exact_frac": round(exact, 4),
+            "ref_interior_depth_exact_frac": round(exact, 4),
             "roofline": roofline_of(kernels, W, H, D, "1080p_d128"),
             "cpu_baseline": None,
         }
@@ -293,9 +310,13 @@ def main():
 
     wl = WORKLOADS[a.workload]
     W, H, D = wl["W"], wl["H"], wl["D"]
-    if "array" in wl:
+    if "rig" in wl:
         return run_array(a, wl, world, rank, local, dev)
     P = a.pairs_per_rank
+    if "total_pairs" in wl:
+        if world > 1 and wl["total_pairs"] % world:
+            raise SystemExit("total_pairs must divide evenly over the ranks")
+        P = wl["total_pairs"] // world
     params = sva.default_params(D=D, dmin=0, dir=-1, subpixel=1)
     ctx = sva.Context(local)
     stream = torch.cuda.Stream(dev)     # non-default stream shared by kernels, copies, RCCL
@@ -304,9 +325,10 @@ def main():
     ctx.reserve(W, H, D)
 
     n_units = world * P   # unit u = pair u, owned by rank u mod world (sdist.shard)
+    seed0 = 0 if "total_pairs" in wl else 1   # config 5 seeds 0-255
     lefts, rights = [], []
     for u in sdist.shard(n_units, rank, world):
-        L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=1 + u)
+        L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=seed0 + u)
         lefts.append(torch.from_numpy(L).to(dev))
         rights.append(torch.from_numpy(R).to(dev))
     disp = torch.zeros((P, H, W), dtype=torch.int16, device=dev)
@@ -343,7 +365,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if "total_pairs" in wl else "weak",
         "vs_baseline": None,
         "dtype": "u16",
         "data": "synthetic (MT19937 u8 texture, 16-stripe piecewise-constant disparity)",

@@ -21,7 +21,10 @@ for step in "$@"; do
     pytest_slow) run pytest_gpu_slow 900 python -m pytest tests -q -m "gpu and slow" ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     pytest_array) run pytest_array 900 python -m pytest tests/test_array_gpu.py -q -m gpu ;;
-    array) run array 600 python bench.py --workload array8 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    array) run center8 600 python bench.py --workload center8 --steps 5 --warmup 2 --no-cpu-baseline
+           run grid8_all 600 python bench.py --workload grid8_all --steps 5 --warmup 2 --no-cpu-baseline ;;
+    batch) run batch256 900 python bench.py --workload batch256_d192 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    array_gloo2) run center8_gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --workload center8 --steps 3 --warmup 1 --dist-backend gloo ;;
     bench4k) run bench4k 600 python bench.py --steps 5 --warmup 2 --workload 4k_d256 --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
