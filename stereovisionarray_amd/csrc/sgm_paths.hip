@@ -51,9 +51,10 @@ struct PathGeom {
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 // Path volumes are written non-temporally (buffer aux bit nt = 2).  Measured
-// (1080p D=128): sgm_paths 0.807 -> 0.593 ms.  With default write-back stores
-// the 2.1 GB of L_r lines displace the 265 MB cost volume that all eight
-// directions re-read; streaming the stores keeps C cache-resident.
+// A/B (1080p D=128, interleaved runs, ablation variants 0/13): sgm_paths
+// 0.826-0.829 -> 0.747-0.774 ms, and the following wta 0.38 -> 0.35 ms.  With
+// default write-back stores the 2.1 GB of L_r lines compete in L2/MALL with
+// the 265 MB cost volume that all eight directions re-read.
 constexpr int kStoreNT = 2;
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, size_t bytes) {
@@ -321,8 +322,8 @@ hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, i
             case 2: hipLaunchKernelGGL((sgm_paths_kernel<8, 2>), grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
             case 3: hipLaunchKernelGGL((sgm_paths_kernel<8, 3>), grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
             case 4: hipLaunchKernelGGL((sgm_paths_kernel<8, 4>), grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
-            case 9: case 10: case 11: case 12: {
-                static const int auxv[4] = {2, 16, 18, 17};
+            case 9: case 10: case 11: case 12: case 13: {
+                static const int auxv[5] = {2, 16, 18, 17, 0};   // 13 = default write-back
                 g.store_aux = auxv[var - 9];
                 hipLaunchKernelGGL((sgm_paths_kernel<8, 9>), grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break; }
             case 5: hipLaunchKernelGGL((sgm_paths_kernel<8, 4>), dim3(2 * g.blk_h), dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
