@@ -333,4 +333,67 @@ inline std::vector<double> disparityToDepth(Engine& eng, const std::vector<uint8
     return depth;
 }
 
+// ---- camera-array pairs ----------
+
+// Match step of the pair (ref, other) on a planar array with grid pitch
+// `pitch` (0.05 m in the reference, CameraStereoVision.cpp:34-39).  Camera
+// `other` sits at grid offset g = round((other.pos3D - ref.pos3D) / pitch);
+// Camera::project (Camera.cpp:15-21) maps a scene point at pixel q of `ref` to
+// q - g * delta in `other`, so the step is -g reduced by the gcd of its
+// components.  k = |major component of g|: the disparity along the major axis
+// is k * delta and the baseline that converts it to depth is k * pitch.
+struct PairStep {
+    int dir = 0, dir_y = 0, k = 0;
+    double baseline = 0.0;
+};
+
+inline PairStep pairStep(const Camera& ref, const Camera& other, double pitch = 0.05) {
+    const int gx = (int)std::lround((other.pos3D.x - ref.pos3D.x) / pitch);
+    const int gy = (int)std::lround((other.pos3D.y - ref.pos3D.y) / pitch);
+    if (gx == 0 && gy == 0) throw Error(SVA_ERR_INVALID_ARG, "pairStep: cameras coincide");
+    int a = std::abs(gx), b = std::abs(gy);
+    while (b) { const int r = a % b; a = b; b = r; }
+    PairStep s;
+    s.dir = -gx / a;
+    s.dir_y = -gy / a;
+    s.k = std::max(std::abs(gx), std::abs(gy));
+    s.baseline = s.k * pitch;
+    return s;
+}
+
+// Mode S on an array pair: base parameters with the pair's step applied.
+inline std::vector<uint16_t> computeDisparityPair(Engine& eng, const ImageView& ref,
+                                                  const ImageView& other, const PairStep& step,
+                                                  sva_sgm_params p) {
+    p.dir = step.dir;
+    p.dir_y = step.dir_y;
+    return computeDisparitySGM(eng, ref, other, p);
+}
+
+// Median depth over the maps of one reference camera, f64,
+// 0 where no map is valid.  maps[i] is W*H u16, baselines[i] its major-axis
+// baseline (PairStep::baseline).
+inline std::vector<double> fuseDepth(Engine& eng, const std::vector<std::vector<uint16_t>>& maps,
+                                     int W, int H, const std::vector<double>& baselines, double f,
+                                     double pixel_size, uint16_t invalid = 0xFFFF,
+                                     std::vector<uint8_t>* n_valid = nullptr) {
+    const size_t np = (size_t)W * H;
+    if (maps.empty() || maps.size() != baselines.size())
+        throw Error(SVA_ERR_INVALID_ARG, "fuseDepth: need one baseline per map");
+    std::vector<uint16_t> packed(np * maps.size());
+    for (size_t i = 0; i < maps.size(); i++) {
+        if (maps[i].size() != np) throw Error(SVA_ERR_INVALID_ARG, "fuseDepth: map size");
+        std::copy(maps[i].begin(), maps[i].end(), packed.begin() + i * np);
+    }
+    std::vector<double> depth(np);
+    uint8_t* nv = nullptr;
+    if (n_valid) {
+        n_valid->resize(np);
+        nv = n_valid->data();
+    }
+    eng.check(sva_fuse_depth(eng.handle(), packed.data(), (int)maps.size(), W, H,
+                             baselines.data(), f, pixel_size, invalid, depth.data(), nv));
+    return depth;
+}
+
 }  // namespace sva

@@ -66,6 +66,18 @@ static void cpu_tests() {
     bool threw = false;
     try { ImageView(a, 2, 2).roi(1, 1, 2, 2); } catch (const Error&) { threw = true; }
     CHECK(threw);
+    // array pair steps on the reference rig (camera 12 at grid (2,2))
+    auto rc = rig(640);
+    PairStep s11 = pairStep(rc[12], rc[11]);   // left neighbour: match at x + d (12 -> 11)
+    CHECK(s11.dir == 1 && s11.dir_y == 0 && s11.k == 1 && std::fabs(s11.baseline - 0.05) < 1e-12);
+    PairStep s18 = pairStep(rc[12], rc[18]);   // (+1,+1) neighbour
+    CHECK(s18.dir == -1 && s18.dir_y == -1 && s18.k == 1);
+    PairStep s7 = pairStep(rc[12], rc[7]);     // above
+    CHECK(s7.dir == 0 && s7.dir_y == 1 && s7.k == 1);
+    PairStep s3 = pairStep(rc[12], rc[3]);     // grid offset (1,-2)
+    CHECK(s3.dir == -1 && s3.dir_y == 2 && s3.k == 2 && std::fabs(s3.baseline - 0.1) < 1e-12);
+    PairStep s14 = pairStep(rc[12], rc[14]);   // (2,0): reduced to a unit step
+    CHECK(s14.dir == -1 && s14.dir_y == 0 && s14.k == 2);
 }
 
 static void gpu_tests() {
@@ -110,6 +122,29 @@ static void gpu_tests() {
         threw = e.status == SVA_ERR_UNSUPPORTED;
     }
     CHECK(threw);
+    // array pair + fusion through the C++ layer: a constant vertical shift d0
+    const int d0 = 9;
+    std::vector<uint8_t> below(W * H);
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) below[y * W + x] = imgs[12][std::min(H - 1, y + d0) * W + x];
+    sva_sgm_params q;
+    sva_sgm_params_default(&q);
+    q.D = 64;
+    PairStep st = pairStep(cams[12], cams[17]);   // camera 17 is one grid row below 12
+    CHECK(st.dir == 0 && st.dir_y == -1);
+    auto dv = computeDisparityPair(eng, views[12], ImageView(below.data(), W, H), st, q);
+    int exact = 0, inner = 0;
+    for (int y = d0 + 20; y < H - 20; y++)
+        for (int x = 8; x < W - 8; x++) {
+            inner++;
+            exact += dv[y * W + x] == d0;
+        }
+    CHECK(exact == inner);
+    std::vector<uint8_t> nv;
+    auto z = fuseDepth(eng, {dv, dv}, W, H, {st.baseline, st.baseline}, cams[12].f,
+                       cams[12].pixel_size, 0xFFFF, &nv);
+    const int pc = (H / 2) * W + W / 2;
+    CHECK(nv[pc] == 2 && z[pc] == (st.baseline * cams[12].f) / ((double)d0 * cams[12].pixel_size));
 }
 
 int main(int argc, char** argv) {
