@@ -151,6 +151,62 @@ int sva_ref_endpoints_d(void* ctx, int width, int height, const sva_camera* ref_
                         const sva_camera* other_cam, int k, double t_near, double t_far,
                         int32_t* ends, uint8_t* valid);
 
+/* ---------------------- refinement and 3-D output --
+ * Semantics of the reference's undefined corners: DESIGN.md §2.7.  Every
+ * u8 plane of a call shares `pitch`; depth planes are dense W*H f64.  Pixels a
+ * routine does not write keep the caller's buffer contents (the reference
+ * leaves them uninitialised). */
+
+/* shiftPerspectiveWithDisparity (functions.cpp:50-72): shifted(x, y) =
+ * image((int)(d*preX + x), (int)(d*preY + y)) for d = disparity(x, y) != 0,
+ * pre = (in.pos - out.pos) / |in.pos - out.pos|. */
+int sva_shift_perspective_d(void* ctx, const sva_camera* in_cam, const sva_camera* out_cam,
+                            const uint8_t* disparity, const uint8_t* image, int width, int height,
+                            size_t pitch, uint8_t* shifted);
+int sva_shift_perspective(void* ctx, const sva_camera* in_cam, const sva_camera* out_cam,
+                          const uint8_t* disparity, const uint8_t* image, int width, int height,
+                          size_t pitch, uint8_t* shifted);
+
+/* improveWithDisparity (functions.cpp:11-48): for each pair i (cam_pairs[2i],
+ * cam_pairs[2i+1], paired image images[i]) shift the image by the disparity,
+ * then re-search 11 candidates along the 0/1 direction with 2k x 2k SADs,
+ * k = (window_size-1)/2 <= 32; the last pair wins.  mask nullable (= the
+ * reference's getFaceMask, :13).  strict: fail with SVA_ERR_INVALID_ARG if a
+ * masked pixel's window leaves the image (the reference's ROI throws);
+ * otherwise such pixels are skipped.  _d: images is a HOST array of device
+ * pointers; the host form takes host pointers. */
+int sva_improve_with_disparity_d(void* ctx, const uint8_t* disparity, const uint8_t* center,
+                                 const uint8_t* const* images, const sva_camera* cam_pairs,
+                                 int n_pairs, int width, int height, size_t pitch,
+                                 const uint8_t* mask, int window_size, int strict, uint8_t* out);
+int sva_improve_with_disparity(void* ctx, const uint8_t* disparity, const uint8_t* center,
+                               const uint8_t* const* images, const sva_camera* cam_pairs,
+                               int n_pairs, int width, int height, size_t pitch,
+                               const uint8_t* mask, int window_size, int strict, uint8_t* out);
+
+/* shiftPerspective2 (functions.cpp:74-97): depth >= 0.5 scattered to
+ * (x + (int)(preX/depth), y + (int)(preY/depth)), pre = (in.pos - out.pos)*f/ps;
+ * collisions resolve to the last write of the reference's x-major loop. */
+int sva_shift_perspective2_d(void* ctx, const sva_camera* in_cam, const sva_camera* out_cam,
+                             const double* depth, int width, int height, double* shifted);
+int sva_shift_perspective2(void* ctx, const sva_camera* in_cam, const sva_camera* out_cam,
+                           const double* depth, int width, int height, double* shifted);
+
+/* Points3DToDepthMap (functions.cpp:118-132): points [n][3] f64 projected
+ * with Camera::project + W/2, H/2; depth = z - cam.z; the last point wins. */
+int sva_points_to_depth_d(void* ctx, const double* points, int64_t n_points,
+                          const sva_camera* cam, int width, int height, double* depth);
+int sva_points_to_depth(void* ctx, const double* points, int64_t n_points,
+                        const sva_camera* cam, int width, int height, double* depth);
+
+/* DepthMapToPoints3D (functions.cpp:134-146): every pixel with depth > 0.1,
+ * in the reference's column-major order, to pos + inv_project(pixel - half)
+ * * depth.  points: capacity width*height*3 f64; *n_points (host) = count. */
+int sva_depth_to_points_d(void* ctx, const double* depth, int width, int height,
+                          const sva_camera* cam, double* points, int64_t* n_points);
+int sva_depth_to_points(void* ctx, const double* depth, int width, int height,
+                        const sva_camera* cam, double* points, int64_t* n_points);
+
 /* Multi-pair depth fusion on the root: per
  * pixel the median of baseline_i * f / (disp_i * pixel_size) over the maps
  * with disp_i != invalid and disp_i > 0 (mean of the middle two for an even

@@ -59,6 +59,14 @@ def _load():
         "svo_wta": (None, [vp, i32, i32, i32, i32, vp, vp]),
         "svo_sgm": (None, [vp, vp, i32, i32, ct.c_ssize_t, i32, i32, i32, i32, i32, vp, vp, i32]),
         "svo_lr_check": (None, [vp, vp, i32, i32, i32, i32, ct.c_uint16]),
+        "svo_step_offset": (None, [i32, i32, i32, P(i32), P(i32)]),
+        "svo_shift_perspective": (None, [P(OCamera), P(OCamera), vp, vp, i32, i32,
+                                         ct.c_ssize_t, vp]),
+        "svo_improve_with_disparity": (i32, [vp, vp, P(vp), P(OCamera), i32, i32, i32,
+                                             ct.c_ssize_t, vp, i32, i32, vp]),
+        "svo_shift_perspective2": (None, [P(OCamera), P(OCamera), vp, i32, i32, vp]),
+        "svo_points_to_depth": (None, [vp, ct.c_int64, P(OCamera), i32, i32, vp]),
+        "svo_depth_to_points": (ct.c_int64, [vp, i32, i32, P(OCamera), vp]),
     }
     for n, (r, a) in sig.items():
         f = getattr(lib, n)
@@ -234,3 +242,55 @@ def fuse_depth(disps, baselines, f, pixel_size, invalid=0xFFFF):
     nv = np.zeros((H, W), np.uint8)
     lib.svo_fuse_depth(_p(d), N, W, H, _p(b), f, pixel_size, invalid, _p(out), _p(nv))
     return out, nv
+
+
+# ---- refinement / 3-D ---------------------------------
+
+def shift_perspective(cin, cout, disp, img, init=None):
+    disp = _c(disp, np.uint8)
+    img = _c(img, np.uint8)
+    H, W = disp.shape
+    out = np.zeros((H, W), np.uint8) if init is None else _c(init, np.uint8).copy()
+    lib.svo_shift_perspective(ct.byref(cin), ct.byref(cout), _p(disp), _p(img), W, H, W, _p(out))
+    return out
+
+
+def improve_with_disparity(disp, center, images, cam_pairs, window=21, mask=None, strict=False,
+                           init=None):
+    """cam_pairs: list of (OCamera, OCamera); returns (status, out)."""
+    disp = _c(disp, np.uint8)
+    center = _c(center, np.uint8)
+    H, W = disp.shape
+    imgs = [_c(i, np.uint8) for i in images]
+    ptrs = (ct.c_void_p * len(imgs))(*[i.ctypes.data for i in imgs])
+    cams = (OCamera * (2 * len(cam_pairs)))()
+    for i, (a, b) in enumerate(cam_pairs):
+        cams[2 * i], cams[2 * i + 1] = a, b
+    out = np.zeros((H, W), np.uint8) if init is None else _c(init, np.uint8).copy()
+    m = None if mask is None else _c(mask, np.uint8)
+    st = lib.svo_improve_with_disparity(_p(disp), _p(center), ptrs, cams, len(imgs), W, H, W,
+                                        _p(m), window, int(strict), _p(out))
+    return st, out
+
+
+def shift_perspective2(cin, cout, depth, init=None):
+    depth = _c(depth, np.float64)
+    H, W = depth.shape
+    out = np.zeros((H, W), np.float64) if init is None else _c(init, np.float64).copy()
+    lib.svo_shift_perspective2(ct.byref(cin), ct.byref(cout), _p(depth), W, H, _p(out))
+    return out
+
+
+def points_to_depth(points, cam, W, H, init=None):
+    pts = _c(points, np.float64).reshape(-1, 3)
+    out = np.zeros((H, W), np.float64) if init is None else _c(init, np.float64).copy()
+    lib.svo_points_to_depth(_p(pts), pts.shape[0], ct.byref(cam), W, H, _p(out))
+    return out
+
+
+def depth_to_points(depth, cam):
+    depth = _c(depth, np.float64)
+    H, W = depth.shape
+    pts = np.zeros((W * H, 3), np.float64)
+    n = lib.svo_depth_to_points(_p(depth), W, H, ct.byref(cam), _p(pts))
+    return pts[:n].copy()

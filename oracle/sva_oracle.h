@@ -141,6 +141,34 @@ void svo_fuse_depth(const uint16_t* disps, int n_maps, int W, int H, const doubl
                     double f, double pixel_size, uint16_t invalid, double* depth,
                     uint8_t* n_valid);
 
+/* --------------------------------------- refinement / 3-D -- */
+/* Semantics for the reference's undefined corners: refine_oracle.c header,
+ * DESIGN.md §2.7.  Pixels a loop skips keep the caller's buffer contents. */
+
+/* shiftPerspectiveWithDisparity (functions.cpp:50-72): gather. */
+void svo_shift_perspective(const svo_camera* in, const svo_camera* out, const uint8_t* disp,
+                           const uint8_t* img, int W, int H, ptrdiff_t pitch, uint8_t* shifted);
+
+/* improveWithDisparity (functions.cpp:11-48); cams = [n][2]; returns 0, or -1
+ * when strict and a masked pixel's window leaves the image (reference throws). */
+int svo_improve_with_disparity(const uint8_t* disp, const uint8_t* center,
+                               const uint8_t* const* images, const svo_camera* cams, int n,
+                               int W, int H, ptrdiff_t pitch, const uint8_t* mask, int window,
+                               int strict, uint8_t* out);
+
+/* shiftPerspective2 (functions.cpp:74-97): scatter, last write in x-major order wins. */
+void svo_shift_perspective2(const svo_camera* in, const svo_camera* out, const double* depth,
+                            int W, int H, double* shifted);
+
+/* Points3DToDepthMap (functions.cpp:118-132): pts [n][3], last point wins. */
+void svo_points_to_depth(const double* pts, int64_t n, const svo_camera* cam, int W, int H,
+                         double* depth);
+
+/* DepthMapToPoints3D (functions.cpp:134-146): column-major, depth > 0.1;
+ * pts capacity W*H*3; returns the count. */
+int64_t svo_depth_to_points(const double* depth, int W, int H, const svo_camera* cam,
+                            double* pts);
+
 #ifdef __cplusplus
 }
 #endif

@@ -35,7 +35,10 @@ EXPORTED = [
     "sva_cost_d", "sva_paths_d", "sva_aggregate_d", "sva_wta_d", "sva_disparity_ref",
     "sva_disparity_ref_d", "sva_ref_endpoints_d", "sva_disparity_to_depth_d",
     "sva_disparity_to_depth", "sva_fuse_depth_d", "sva_fuse_depth",
-    "sva_batch_sgm",
+    "sva_shift_perspective_d", "sva_shift_perspective", "sva_improve_with_disparity_d",
+    "sva_improve_with_disparity", "sva_shift_perspective2_d", "sva_shift_perspective2",
+    "sva_points_to_depth_d", "sva_points_to_depth", "sva_depth_to_points_d",
+    "sva_depth_to_points", "sva_batch_sgm",
 ]
 
 
@@ -130,6 +133,18 @@ def _load() -> ct.CDLL:
         "sva_disparity_to_depth": (i32, [vp, vp, i32, dbl, dbl, dbl, vp]),
         "sva_fuse_depth_d": (i32, [vp, vp, i32, i32, i32, P(dbl), dbl, dbl, ct.c_uint16, vp, vp]),
         "sva_fuse_depth": (i32, [vp, vp, i32, i32, i32, P(dbl), dbl, dbl, ct.c_uint16, vp, vp]),
+        "sva_shift_perspective_d": (i32, [vp, P(Camera), P(Camera), vp, vp, i32, i32, sz, vp]),
+        "sva_shift_perspective": (i32, [vp, P(Camera), P(Camera), vp, vp, i32, i32, sz, vp]),
+        "sva_improve_with_disparity_d": (i32, [vp, vp, vp, P(vp), P(Camera), i32, i32, i32, sz,
+                                               vp, i32, i32, vp]),
+        "sva_improve_with_disparity": (i32, [vp, vp, vp, P(vp), P(Camera), i32, i32, i32, sz,
+                                             vp, i32, i32, vp]),
+        "sva_shift_perspective2_d": (i32, [vp, P(Camera), P(Camera), vp, i32, i32, vp]),
+        "sva_shift_perspective2": (i32, [vp, P(Camera), P(Camera), vp, i32, i32, vp]),
+        "sva_points_to_depth_d": (i32, [vp, vp, ct.c_int64, P(Camera), i32, i32, vp]),
+        "sva_points_to_depth": (i32, [vp, vp, ct.c_int64, P(Camera), i32, i32, vp]),
+        "sva_depth_to_points_d": (i32, [vp, vp, i32, i32, P(Camera), vp, P(ct.c_int64)]),
+        "sva_depth_to_points": (i32, [vp, vp, i32, i32, P(Camera), vp, P(ct.c_int64)]),
         "sva_batch_sgm": (i32, [P(vp), i32, P(PairJob), i32, P(SgmParams)]),
     }
     for name, (res, args) in sig.items():
@@ -280,6 +295,73 @@ class Context:
     def ref_endpoints_d(self, W, H, cref, coth, k, t_near, t_far, ends, valid):
         self._chk(lib.sva_ref_endpoints_d(self.h, W, H, ct.byref(cref), ct.byref(coth), k,
                                           t_near, t_far, _ptr(ends), _ptr(valid)))
+
+    # -- refinement / 3-D, host arrays
+    def shift_perspective(self, cin: Camera, cout: Camera, disp, image, init=None):
+        disp = np.ascontiguousarray(disp, dtype=np.uint8)
+        image = np.ascontiguousarray(image, dtype=np.uint8)
+        H, W = disp.shape
+        out = np.zeros((H, W), np.uint8) if init is None else np.array(init, np.uint8)
+        self._chk(lib.sva_shift_perspective(self.h, ct.byref(cin), ct.byref(cout), _ptr(disp),
+                                            _ptr(image), W, H, W, _ptr(out)))
+        return out
+
+    def improve_with_disparity(self, disp, center, images, cam_pairs, window=21, mask=None,
+                               strict=False, init=None):
+        disp = np.ascontiguousarray(disp, dtype=np.uint8)
+        center = np.ascontiguousarray(center, dtype=np.uint8)
+        H, W = disp.shape
+        imgs = [np.ascontiguousarray(i, dtype=np.uint8) for i in images]
+        ptrs = (ct.c_void_p * max(1, len(imgs)))(*[i.ctypes.data for i in imgs])
+        cams = (Camera * max(1, 2 * len(cam_pairs)))()
+        for i, (a, b) in enumerate(cam_pairs):
+            cams[2 * i], cams[2 * i + 1] = a, b
+        out = np.zeros((H, W), np.uint8) if init is None else np.array(init, np.uint8)
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        self._chk(lib.sva_improve_with_disparity(self.h, _ptr(disp), _ptr(center), ptrs, cams,
+                                                 len(imgs), W, H, W, _ptr(m), window,
+                                                 int(strict), _ptr(out)))
+        return out
+
+    def improve_with_disparity_d(self, disp, center, images, cam_pairs, W, H, pitch, mask,
+                                 window, strict, out):
+        ptrs = (ct.c_void_p * max(1, len(images)))(*images)
+        cams = (Camera * max(1, 2 * len(cam_pairs)))()
+        for i, (a, b) in enumerate(cam_pairs):
+            cams[2 * i], cams[2 * i + 1] = a, b
+        self._chk(lib.sva_improve_with_disparity_d(self.h, _ptr(disp), _ptr(center), ptrs, cams,
+                                                   len(images), W, H, pitch, _ptr(mask), window,
+                                                   int(strict), _ptr(out)))
+
+    def shift_perspective2(self, cin: Camera, cout: Camera, depth, init=None):
+        depth = np.ascontiguousarray(depth, dtype=np.float64)
+        H, W = depth.shape
+        out = np.zeros((H, W), np.float64) if init is None else np.array(init, np.float64)
+        self._chk(lib.sva_shift_perspective2(self.h, ct.byref(cin), ct.byref(cout), _ptr(depth),
+                                             W, H, _ptr(out)))
+        return out
+
+    def points_to_depth(self, points, cam: Camera, W, H, init=None):
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+        out = np.zeros((H, W), np.float64) if init is None else np.array(init, np.float64)
+        self._chk(lib.sva_points_to_depth(self.h, _ptr(pts), pts.shape[0], ct.byref(cam), W, H,
+                                          _ptr(out)))
+        return out
+
+    def depth_to_points(self, depth, cam: Camera):
+        depth = np.ascontiguousarray(depth, dtype=np.float64)
+        H, W = depth.shape
+        pts = np.zeros((W * H, 3), np.float64)
+        n = ct.c_int64(0)
+        self._chk(lib.sva_depth_to_points(self.h, _ptr(depth), W, H, ct.byref(cam), _ptr(pts),
+                                          ct.byref(n)))
+        return pts[:n.value].copy()
+
+    def depth_to_points_d(self, depth, W, H, cam: Camera, points) -> int:
+        n = ct.c_int64(0)
+        self._chk(lib.sva_depth_to_points_d(self.h, _ptr(depth), W, H, ct.byref(cam),
+                                            _ptr(points), ct.byref(n)))
+        return n.value
 
     def fuse_depth(self, disps: np.ndarray, baselines, f, pixel_size, invalid=0xFFFF):
         d = np.ascontiguousarray(disps, dtype=np.uint16)

@@ -11,6 +11,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -214,6 +215,56 @@ int check_ref_args(Ctx* c, int W, int H, int k, double t_near, double t_far) {
     return SVA_OK;
 }
 
+// refinement / 3-D helpers
+
+int check_planes(Ctx* c, int W, int H, size_t pitch) {
+    if (W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "image size must be positive");
+    if (pitch < (size_t)W) return fail(c, SVA_ERR_INVALID_ARG, "pitch smaller than width");
+    if ((long long)W * H > (1ll << 31) - 1) return fail(c, SVA_ERR_INVALID_ARG, "image too large");
+    return SVA_OK;
+}
+
+int check_window(Ctx* c, int window_size) {
+    if (window_size < 1 || (window_size - 1) / 2 > 32)
+        return fail(c, SVA_ERR_UNSUPPORTED, "window_size must give kernelSize (w-1)/2 in 0..32");
+    return SVA_OK;
+}
+
+// improveWithDisparity on device planes; images = n device pointers.
+int run_improve(Ctx* c, const uint8_t* disp, const uint8_t* center, const uint8_t* const* images,
+                const sva_camera* cams, int n, int W, int H, size_t pitch, const uint8_t* mask,
+                int window_size, int strict, uint8_t* out,
+                const std::function<int(int, const uint8_t**)>& fetch) {
+    const size_t bytes = (size_t)H * pitch;
+    SVA_HIP(c, c->shifted.ensure(bytes), "shift workspace");
+    SVA_HIP(c, c->total.ensure(sizeof(long long)), "fault flag");
+    int* fault = (int*)c->total.ptr;
+    SVA_HIP(c, hipMemsetAsync(fault, 0, sizeof(int), c->stream), "memset");
+    uint8_t* sh = (uint8_t*)c->shifted.ptr;
+    const int k = (window_size - 1) / 2;
+    for (int i = 0; i < n; i++) {
+        const uint8_t* img = images ? images[i] : nullptr;
+        int s;
+        if (fetch && (s = fetch(i, &img))) return s;
+        // the reference's shifted Mat is uninitialised; DESIGN.md §2.7 fixes it to 0
+        SVA_HIP(c, hipMemsetAsync(sh, 0, bytes, c->stream), "memset");
+        SVA_HIP(c, launch_shift_perspective(*c, cams[2 * i], cams[2 * i + 1], disp, img, W, H,
+                                            pitch, sh), "shift launch");
+        SVA_HIP(c, launch_refine(*c, disp, center, sh, mask, W, H, pitch, k, cams[2 * i],
+                                 cams[2 * i + 1], out, fault), "refine launch");
+    }
+    if (strict) {
+        int f = 0;
+        SVA_HIP(c, hipMemcpyAsync(&f, fault, sizeof(int), hipMemcpyDeviceToHost, c->stream),
+                "download");
+        SVA_HIP(c, hipStreamSynchronize(c->stream), "sync");
+        if (f)
+            return fail(c, SVA_ERR_INVALID_ARG,
+                        "a masked pixel's window leaves the image (the reference's ROI throws)");
+    }
+    return SVA_OK;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ ABI --
@@ -283,7 +334,7 @@ int sva_destroy(void* ctx) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->census_l, &c->census_r, &c->cost, &c->paths, &c->scratch_u16,
                       &c->disp_r, &c->in_a, &c->in_b, &c->in_mask, &c->out_a, &c->out_b,
-                      &c->out_c})
+                      &c->out_c, &c->in_c, &c->shifted, &c->keys, &c->counts, &c->total})
         b->release();
     c->timer.release_all();
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -596,6 +647,231 @@ int sva_fuse_depth(void* ctx, const uint16_t* disps, int n_maps, int W, int H,
         SVA_HIP(c, hipMemcpyAsync(n_valid, c->out_b.ptr, np, hipMemcpyDeviceToHost, c->stream),
                 "download");
     SVA_HIP(c, hipStreamSynchronize(c->stream), "sync");
+    return SVA_OK;
+}
+
+// ------------------------------------------ refinement / 3-D --
+int sva_shift_perspective_d(void* ctx, const sva_camera* in_cam, const sva_camera* out_cam,
+                            const uint8_t* disparity, const uint8_t* image, int W, int H,
+                            size_t pitch, uint8_t* shifted) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_planes(c, W, H, pitch)) || (s = check_camera(c, in_cam)) ||
+        (s = check_camera(c, out_cam)))
+        return s;
+    if (!disparity || !image || !shifted) return fail(c, SVA_ERR_INVALID_ARG, "null plane");
+    SVA_HIP(c, launch_shift_perspective(*c, *in_cam, *out_cam, disparity, image, W, H, pitch,
+                                        shifted), "shift launch");
+    return SVA_OK;
+}
+
+int sva_shift_perspective(void* ctx, const sva_camera* in_cam, const sva_camera* out_cam,
+                          const uint8_t* disparity, const uint8_t* image, int W, int H,
+                          size_t pitch, uint8_t* shifted) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_planes(c, W, H, pitch)) || (s = check_camera(c, in_cam)) ||
+        (s = check_camera(c, out_cam)))
+        return s;
+    if (!disparity || !image || !shifted) return fail(c, SVA_ERR_INVALID_ARG, "null plane");
+    const size_t bytes = (size_t)H * pitch;
+    SVA_HIP(c, c->in_a.ensure(bytes), "staging");
+    SVA_HIP(c, c->in_b.ensure(bytes), "staging");
+    SVA_HIP(c, c->out_a.ensure(bytes), "staging");
+    hipStream_t st = c->stream;
+    SVA_HIP(c, hipMemcpyAsync(c->in_a.ptr, disparity, bytes, hipMemcpyHostToDevice, st), "upload");
+    SVA_HIP(c, hipMemcpyAsync(c->in_b.ptr, image, bytes, hipMemcpyHostToDevice, st), "upload");
+    SVA_HIP(c, hipMemcpyAsync(c->out_a.ptr, shifted, bytes, hipMemcpyHostToDevice, st), "upload");
+    SVA_HIP(c, launch_shift_perspective(*c, *in_cam, *out_cam, (uint8_t*)c->in_a.ptr,
+                                        (uint8_t*)c->in_b.ptr, W, H, pitch,
+                                        (uint8_t*)c->out_a.ptr), "shift launch");
+    SVA_HIP(c, hipMemcpyAsync(shifted, c->out_a.ptr, bytes, hipMemcpyDeviceToHost, st), "download");
+    SVA_HIP(c, hipStreamSynchronize(st), "sync");
+    return SVA_OK;
+}
+
+int sva_improve_with_disparity_d(void* ctx, const uint8_t* disparity, const uint8_t* center,
+                                 const uint8_t* const* images, const sva_camera* cam_pairs,
+                                 int n_pairs, int W, int H, size_t pitch, const uint8_t* mask,
+                                 int window_size, int strict, uint8_t* out) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_planes(c, W, H, pitch)) || (s = check_window(c, window_size))) return s;
+    if (n_pairs < 0 || (n_pairs > 0 && (!images || !cam_pairs)))
+        return fail(c, SVA_ERR_INVALID_ARG, "bad pair list");
+    if (!disparity || !center || !out) return fail(c, SVA_ERR_INVALID_ARG, "null plane");
+    for (int i = 0; i < n_pairs; i++)
+        if (!images[i]) return fail(c, SVA_ERR_INVALID_ARG, "null pair image");
+    return run_improve(c, disparity, center, images, cam_pairs, n_pairs, W, H, pitch, mask,
+                       window_size, strict, out, nullptr);
+}
+
+int sva_improve_with_disparity(void* ctx, const uint8_t* disparity, const uint8_t* center,
+                               const uint8_t* const* images, const sva_camera* cam_pairs,
+                               int n_pairs, int W, int H, size_t pitch, const uint8_t* mask,
+                               int window_size, int strict, uint8_t* out) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_planes(c, W, H, pitch)) || (s = check_window(c, window_size))) return s;
+    if (n_pairs < 0 || (n_pairs > 0 && (!images || !cam_pairs)))
+        return fail(c, SVA_ERR_INVALID_ARG, "bad pair list");
+    if (!disparity || !center || !out) return fail(c, SVA_ERR_INVALID_ARG, "null plane");
+    for (int i = 0; i < n_pairs; i++)
+        if (!images[i]) return fail(c, SVA_ERR_INVALID_ARG, "null pair image");
+    const size_t bytes = (size_t)H * pitch;
+    SVA_HIP(c, c->in_a.ensure(bytes), "staging");
+    SVA_HIP(c, c->in_b.ensure(bytes), "staging");
+    SVA_HIP(c, c->in_c.ensure(bytes), "staging");
+    SVA_HIP(c, c->out_a.ensure(bytes), "staging");
+    if (mask) SVA_HIP(c, c->in_mask.ensure(bytes), "staging");
+    hipStream_t st = c->stream;
+    SVA_HIP(c, hipMemcpyAsync(c->in_a.ptr, disparity, bytes, hipMemcpyHostToDevice, st), "upload");
+    SVA_HIP(c, hipMemcpyAsync(c->in_b.ptr, center, bytes, hipMemcpyHostToDevice, st), "upload");
+    if (mask) SVA_HIP(c, hipMemcpyAsync(c->in_mask.ptr, mask, bytes, hipMemcpyHostToDevice, st), "upload");
+    // pixels the refinement does not reach keep the caller's values
+    SVA_HIP(c, hipMemcpyAsync(c->out_a.ptr, out, bytes, hipMemcpyHostToDevice, st), "upload");
+    uint8_t* dimg = (uint8_t*)c->in_c.ptr;
+    auto fetch = [&](int i, const uint8_t** img) -> int {
+        // one staging buffer reused per pair: stream order keeps the upload
+        // of pair i behind pair i-1's kernels
+        SVA_HIP(c, hipMemcpyAsync(dimg, images[i], bytes, hipMemcpyHostToDevice, st), "upload");
+        *img = dimg;
+        return SVA_OK;
+    };
+    if ((s = run_improve(c, (uint8_t*)c->in_a.ptr, (uint8_t*)c->in_b.ptr, nullptr, cam_pairs,
+                         n_pairs, W, H, pitch, mask ? (uint8_t*)c->in_mask.ptr : nullptr,
+                         window_size, strict, (uint8_t*)c->out_a.ptr, fetch)))
+        return s;
+    SVA_HIP(c, hipMemcpyAsync(out, c->out_a.ptr, bytes, hipMemcpyDeviceToHost, st), "download");
+    SVA_HIP(c, hipStreamSynchronize(st), "sync");
+    return SVA_OK;
+}
+
+int sva_shift_perspective2_d(void* ctx, const sva_camera* in_cam, const sva_camera* out_cam,
+                             const double* depth, int W, int H, double* shifted) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_planes(c, W, H, (size_t)W)) || (s = check_camera(c, in_cam)) ||
+        (s = check_camera(c, out_cam)))
+        return s;
+    if (!depth || !shifted) return fail(c, SVA_ERR_INVALID_ARG, "null plane");
+    SVA_HIP(c, c->keys.ensure((size_t)W * H * 4), "key workspace");
+    SVA_HIP(c, launch_shift_perspective2(*c, *in_cam, *out_cam, depth, W, H,
+                                         (unsigned*)c->keys.ptr, shifted), "shift2 launch");
+    return SVA_OK;
+}
+
+int sva_shift_perspective2(void* ctx, const sva_camera* in_cam, const sva_camera* out_cam,
+                           const double* depth, int W, int H, double* shifted) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_planes(c, W, H, (size_t)W)) || (s = check_camera(c, in_cam)) ||
+        (s = check_camera(c, out_cam)))
+        return s;
+    if (!depth || !shifted) return fail(c, SVA_ERR_INVALID_ARG, "null plane");
+    const size_t bytes = (size_t)W * H * 8;
+    SVA_HIP(c, c->in_a.ensure(bytes), "staging");
+    SVA_HIP(c, c->out_a.ensure(bytes), "staging");
+    SVA_HIP(c, c->keys.ensure((size_t)W * H * 4), "key workspace");
+    hipStream_t st = c->stream;
+    SVA_HIP(c, hipMemcpyAsync(c->in_a.ptr, depth, bytes, hipMemcpyHostToDevice, st), "upload");
+    SVA_HIP(c, hipMemcpyAsync(c->out_a.ptr, shifted, bytes, hipMemcpyHostToDevice, st), "upload");
+    SVA_HIP(c, launch_shift_perspective2(*c, *in_cam, *out_cam, (double*)c->in_a.ptr, W, H,
+                                         (unsigned*)c->keys.ptr, (double*)c->out_a.ptr),
+            "shift2 launch");
+    SVA_HIP(c, hipMemcpyAsync(shifted, c->out_a.ptr, bytes, hipMemcpyDeviceToHost, st), "download");
+    SVA_HIP(c, hipStreamSynchronize(st), "sync");
+    return SVA_OK;
+}
+
+int sva_points_to_depth_d(void* ctx, const double* points, int64_t n_points,
+                          const sva_camera* cam, int W, int H, double* depth) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_planes(c, W, H, (size_t)W)) || (s = check_camera(c, cam))) return s;
+    if (n_points < 0 || n_points > 0xfffffffell || (n_points > 0 && !points) || !depth)
+        return fail(c, SVA_ERR_INVALID_ARG, "bad point list");
+    SVA_HIP(c, c->keys.ensure((size_t)W * H * 4), "key workspace");
+    SVA_HIP(c, launch_points_to_depth(*c, points, n_points, *cam, W, H, (unsigned*)c->keys.ptr,
+                                      depth), "points launch");
+    return SVA_OK;
+}
+
+int sva_points_to_depth(void* ctx, const double* points, int64_t n_points, const sva_camera* cam,
+                        int W, int H, double* depth) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_planes(c, W, H, (size_t)W)) || (s = check_camera(c, cam))) return s;
+    if (n_points < 0 || n_points > 0xfffffffell || (n_points > 0 && !points) || !depth)
+        return fail(c, SVA_ERR_INVALID_ARG, "bad point list");
+    const size_t pbytes = (size_t)n_points * 24, dbytes = (size_t)W * H * 8;
+    SVA_HIP(c, c->in_a.ensure(pbytes ? pbytes : 8), "staging");
+    SVA_HIP(c, c->out_a.ensure(dbytes), "staging");
+    SVA_HIP(c, c->keys.ensure((size_t)W * H * 4), "key workspace");
+    hipStream_t st = c->stream;
+    if (pbytes)
+        SVA_HIP(c, hipMemcpyAsync(c->in_a.ptr, points, pbytes, hipMemcpyHostToDevice, st), "upload");
+    SVA_HIP(c, hipMemcpyAsync(c->out_a.ptr, depth, dbytes, hipMemcpyHostToDevice, st), "upload");
+    SVA_HIP(c, launch_points_to_depth(*c, (double*)c->in_a.ptr, n_points, *cam, W, H,
+                                      (unsigned*)c->keys.ptr, (double*)c->out_a.ptr),
+            "points launch");
+    SVA_HIP(c, hipMemcpyAsync(depth, c->out_a.ptr, dbytes, hipMemcpyDeviceToHost, st), "download");
+    SVA_HIP(c, hipStreamSynchronize(st), "sync");
+    return SVA_OK;
+}
+
+int sva_depth_to_points_d(void* ctx, const double* depth, int W, int H, const sva_camera* cam,
+                          double* points, int64_t* n_points) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_planes(c, W, H, (size_t)W)) || (s = check_camera(c, cam))) return s;
+    if (!depth || !points || !n_points) return fail(c, SVA_ERR_INVALID_ARG, "null argument");
+    SVA_HIP(c, c->counts.ensure(d2p_units(W, H) * 4), "count workspace");
+    SVA_HIP(c, c->total.ensure(sizeof(long long)), "count workspace");
+    SVA_HIP(c, launch_depth_to_points(*c, depth, W, H, *cam, (unsigned*)c->counts.ptr,
+                                      (long long*)c->total.ptr, points), "d2p launch");
+    long long n = 0;
+    SVA_HIP(c, hipMemcpyAsync(&n, c->total.ptr, sizeof(n), hipMemcpyDeviceToHost, c->stream),
+            "download");
+    SVA_HIP(c, hipStreamSynchronize(c->stream), "sync");
+    *n_points = n;
+    return SVA_OK;
+}
+
+int sva_depth_to_points(void* ctx, const double* depth, int W, int H, const sva_camera* cam,
+                        double* points, int64_t* n_points) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_planes(c, W, H, (size_t)W)) || (s = check_camera(c, cam))) return s;
+    if (!depth || !points || !n_points) return fail(c, SVA_ERR_INVALID_ARG, "null argument");
+    const size_t np = (size_t)W * H;
+    SVA_HIP(c, c->in_a.ensure(np * 8), "staging");
+    SVA_HIP(c, c->out_a.ensure(np * 24), "staging");
+    SVA_HIP(c, c->counts.ensure(d2p_units(W, H) * 4), "count workspace");
+    SVA_HIP(c, c->total.ensure(sizeof(long long)), "count workspace");
+    hipStream_t st = c->stream;
+    SVA_HIP(c, hipMemcpyAsync(c->in_a.ptr, depth, np * 8, hipMemcpyHostToDevice, st), "upload");
+    SVA_HIP(c, launch_depth_to_points(*c, (double*)c->in_a.ptr, W, H, *cam,
+                                      (unsigned*)c->counts.ptr, (long long*)c->total.ptr,
+                                      (double*)c->out_a.ptr), "d2p launch");
+    long long n = 0;
+    SVA_HIP(c, hipMemcpyAsync(&n, c->total.ptr, sizeof(n), hipMemcpyDeviceToHost, st), "download");
+    SVA_HIP(c, hipStreamSynchronize(st), "sync");
+    if (n > 0)
+        SVA_HIP(c, hipMemcpyAsync(points, c->out_a.ptr, (size_t)n * 24, hipMemcpyDeviceToHost, st),
+                "download");
+    SVA_HIP(c, hipStreamSynchronize(st), "sync");
+    *n_points = n;
     return SVA_OK;
 }
 

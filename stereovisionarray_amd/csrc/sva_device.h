@@ -74,4 +74,32 @@ __device__ __forceinline__ int2 step_offset(int s, int bx, int by) {
     return make_int2(bx < 0 ? -mx : (bx > 0 ? mx : 0), by < 0 ? -my : (by > 0 ? my : 0));
 }
 
+// Sum |a-b| over one 2k-byte row pair.  ND = ceil(2k/4) dwords; `lastmask`
+// keeps the valid bytes of the final dword (0xffff when 2k % 4 == 2).
+template <int ND>
+__device__ __forceinline__ unsigned sad_row(const uint8_t* a, const uint8_t* b, unsigned lastmask,
+                                            int nbytes, unsigned acc) {
+    const uintptr_t ua = (uintptr_t)a, ub = (uintptr_t)b;
+    const unsigned* wa = (const unsigned*)(ua & ~(uintptr_t)3);
+    const unsigned* wb = (const unsigned*)(ub & ~(uintptr_t)3);
+    const unsigned sa = (unsigned)(ua & 3), sb = (unsigned)(ub & 3);
+    // Never touch a dword past the one holding the last valid byte.
+    const int la = (int)(((ua + nbytes - 1) & ~(uintptr_t)3) - (ua & ~(uintptr_t)3)) >> 2;
+    const int lb = (int)(((ub + nbytes - 1) & ~(uintptr_t)3) - (ub & ~(uintptr_t)3)) >> 2;
+    unsigned ra[ND + 1], rb[ND + 1];
+#pragma unroll
+    for (int j = 0; j <= ND; j++) {
+        ra[j] = wa[j < la ? j : la];
+        rb[j] = wb[j < lb ? j : lb];
+    }
+#pragma unroll
+    for (int j = 0; j < ND; j++) {
+        unsigned oa = __builtin_amdgcn_alignbyte(ra[j + 1], ra[j], sa);
+        unsigned ob = __builtin_amdgcn_alignbyte(rb[j + 1], rb[j], sb);
+        if (j == ND - 1) { oa &= lastmask; ob &= lastmask; }
+        acc = __builtin_amdgcn_sad_u8(oa, ob, acc);
+    }
+    return acc;
+}
+
 }  // namespace sva

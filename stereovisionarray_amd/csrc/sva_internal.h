@@ -56,6 +56,8 @@ struct Ctx {
     DevBuf census_l, census_r, cost, paths, scratch_u16, disp_r;
     // host-pointer staging
     DevBuf in_a, in_b, in_mask, out_a, out_b, out_c;
+    // refinement / 3-D workspace (refine.hip)
+    DevBuf in_c, shifted, keys, counts, total;
     int cu_count = 256;
 };
 
@@ -111,6 +113,23 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
                             const uint8_t* valid_in, int k, uint8_t* disp_u8,
                             uint16_t* disp_u16, uint8_t* valid_out);
 // depth.hip
+// refine.hip
+hipError_t launch_shift_perspective(Ctx& c, const sva_camera& in, const sva_camera& out,
+                                    const uint8_t* disp, const uint8_t* img, int W, int H,
+                                    size_t pitch, uint8_t* shifted);
+hipError_t launch_refine(Ctx& c, const uint8_t* disp, const uint8_t* center,
+                         const uint8_t* shifted, const uint8_t* mask, int W, int H, size_t pitch,
+                         int k, const sva_camera& c0, const sva_camera& c1, uint8_t* out,
+                         int* fault);
+hipError_t launch_shift_perspective2(Ctx& c, const sva_camera& in, const sva_camera& out,
+                                     const double* depth, int W, int H, unsigned* keys,
+                                     double* shifted);
+hipError_t launch_points_to_depth(Ctx& c, const double* pts, long long n, const sva_camera& cam,
+                                  int W, int H, unsigned* keys, double* depth);
+size_t d2p_units(int W, int H);
+hipError_t launch_depth_to_points(Ctx& c, const double* depth, int W, int H,
+                                  const sva_camera& cam, unsigned* counts, long long* total,
+                                  double* pts);
 hipError_t launch_disp_to_depth(Ctx& c, const uint8_t* disp, int n, double cam_distance,
                                 double f, double pixel_size, double* depth);
 

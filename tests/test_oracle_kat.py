@@ -303,3 +303,82 @@ def test_step_offset_kat(oracle):
     for bx, by in [(2, 1), (-3, -2), (1, -4), (0, 2), (7, 7)]:
         for s in range(0, 300, 7):
             assert oracle.step_offset(s, bx, by) == tuple(int(v) for v in synth.step_offset(s, bx, by))
+
+
+# ---- refinement / 3-D, hand-derived ---------------------
+
+def _cam(oracle, f, pos, ps):
+    return oracle.OCamera.make(f, pos, ps)
+
+
+def test_shift_perspective_kat(oracle):
+    """functions.cpp:50-72: pre = (in - out) / |in - out|; gather at
+    ((int)(d*preX + x), (int)(d*preY + y)); d == 0 and out-of-range keep init."""
+    c12 = _cam(oracle, 0.05, (0, 0, -0.75), 1e-4)
+    c11 = _cam(oracle, 0.05, (-0.05, 0, -0.75), 1e-4)
+    d = np.array([[0, 2, 1, 5]], np.uint8)
+    img = np.array([[10, 20, 30, 40]], np.uint8)
+    out = oracle.shift_perspective(c12, c11, d, img, init=np.full((1, 4), 7, np.uint8))
+    assert out[0].tolist() == [7, 40, 40, 7]     # x=3: 3+5 outside -> untouched
+    c6 = _cam(oracle, 0.05, (-0.05, -0.05, -0.75), 1e-4)   # diagonal: pre = (1/sqrt2, 1/sqrt2)
+    d = np.zeros((4, 4), np.uint8); d[0, 0] = 3            # 3/sqrt2 = 2.12 -> (2, 2)
+    img = np.arange(16, dtype=np.uint8).reshape(4, 4)
+    assert oracle.shift_perspective(c12, c6, d, img)[0, 0] == img[2, 2]
+
+
+def test_improve_with_disparity_kat(oracle):
+    """functions.cpp:11-48 by construction: with disp = d0 and the paired image
+    img(x) = centre(x - d0 - 2), the shifted image is centre(x - 2), so
+    candidate p = 7 matches exactly and the refined disparity is d0 + 2."""
+    W, H, d0 = 64, 24, 6
+    center = synth.texture(H, W, 3)
+    img = np.zeros_like(center)
+    img[:, d0 + 2:] = center[:, : W - d0 - 2]
+    c0 = _cam(oracle, 0.05, (0.05, 0, -0.75), 1e-4)   # c0 - c1 = (+0.05, 0): ddx = 1, pre = (1, 0)
+    c1 = _cam(oracle, 0.05, (0.0, 0, -0.75), 1e-4)
+    disp = np.full((H, W), d0, np.uint8)
+    mask = np.zeros((H, W), np.uint8)
+    mask[6:18, 20:40] = 1
+    st, out = oracle.improve_with_disparity(disp, center, [img], [(c0, c1)], window=7, mask=mask)
+    assert st == 0
+    assert (out[6:18, 20:40] == d0 + 2).all() and (out[mask == 0] == 0).all()
+    # disp = 0: nothing shifts (shifted stays 0), all 11 SADs tie -> first
+    # candidate p = 0 -> 0 + (0 - 5) * 1 = -5 -> (uchar)(int) wraps to 251
+    st, out = oracle.improve_with_disparity(np.zeros((H, W), np.uint8), center, [img],
+                                            [(c0, c1)], window=7, mask=mask)
+    assert (out[6:18, 20:40] == 251).all()
+    # other camera at +x (c0 - c1 < 0): direction (0, 0) -> disparity unchanged
+    st, out = oracle.improve_with_disparity(disp, center, [img], [(c1, c0)], window=7, mask=mask)
+    assert (out[6:18, 20:40] == d0).all()
+    # strict: a masked pixel whose window leaves the image fails like the ROI throw
+    m2 = mask.copy(); m2[0, 0] = 1
+    st, _ = oracle.improve_with_disparity(disp, center, [img], [(c0, c1)], window=7, mask=m2,
+                                          strict=True)
+    assert st == -1
+
+
+def test_shift_perspective2_kat(oracle):
+    """functions.cpp:74-97: preX = 0.05*0.05/1e-3 = 2.5 (to f64 rounding);
+    depth 1 at x=0 -> +int(2.5) = 2; depth 2 at x=1 -> +int(1.25) = 1: both
+    land on x=2, the later x (loop order) wins; depth < 0.5 skipped."""
+    cin = _cam(oracle, 0.05, (0.05, 0, 0), 1e-3)
+    cout = _cam(oracle, 0.05, (0.0, 0, 0), 1e-3)
+    depth = np.array([[1.0, 2.0, 0.4, 0.0, 0.0]], np.float64)
+    out = oracle.shift_perspective2(cin, cout, depth)
+    assert out[0].tolist() == [0.0, 0.0, 2.0, 0.0, 0.0]
+
+
+def test_points_depth_kat(oracle):
+    """functions.cpp:118-146 with f = ps = 1 at the origin, 4x4 (half = 2)."""
+    cam = _cam(oracle, 1.0, (0, 0, 0), 1.0)
+    pts = np.array([[1, 1, 2], [-1.9, 0, 1], [0, 0, 5], [0.4, 0, 2], [0, 0, 0]], np.float64)
+    d = oracle.points_to_depth(pts, cam, 4, 4)
+    # (1,1,2): mult .5 -> (0,0)+2 = (2,2) z=2; (-1.9,0,1): (int)-1.9 = -1 -> (1,2);
+    # (0,0,5) -> (2,2) z=5; (0.4,0,2): (int)0.2 = 0 -> (2,2) z=2 (last wins);
+    # (0,0,0): z - cz = 0 -> mult inf -> 0*inf = NaN -> skipped
+    assert d[2, 2] == 2.0 and d[2, 1] == 1.0 and np.count_nonzero(d) == 2
+    depth = np.array([[0.0, 1.0], [0.05, 2.0]])
+    p = oracle.depth_to_points(depth, cam)          # column-major: u=1 v=0, then u=1 v=1
+    r = 1 / np.sqrt(2.0)
+    assert p.shape == (2, 3)
+    assert np.allclose(p[0], [0, -r, r], atol=0, rtol=1e-15) and p[1].tolist() == [0, 0, 2]
