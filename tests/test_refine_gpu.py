@@ -182,8 +182,9 @@ def test_depth_to_points(ctx, sva, oracle, W, H):
 def test_depth_points_round_trip(ctx, sva):
     """Points3DToDepthMap(DepthMapToPoints3D(depth)) at constant depth 1: every
     pixel becomes one point; re-projection lands on the pixel or (truncation
-    of x.9999) a neighbour, and the depth it carries is r_z of the source ray
-    -- within 1e-6 of r_z at the landing pixel."""
+    of x.9999) a neighbour, and the depth it carries is r_z of the source ray,
+    which differs from r_z at the landing pixel by at most ~1.6e-3 relative
+    (one pixel's change of the ray angle at the frame edge)."""
     W, H = 320, 240
     cams = synth.reference_array(0.036 / W)
     cam = sva.Camera.make(*cams[12])
@@ -195,4 +196,5 @@ def test_depth_points_round_trip(ctx, sva):
     u, v = np.meshgrid(np.arange(W) - W // 2, np.arange(H) - H // 2)
     ps, f = cams[12][2], cams[12][0]
     rz = f / np.sqrt((u * ps) ** 2 + (v * ps) ** 2 + f * f)
-    assert np.allclose(back[hit], rz[hit], rtol=1e-6, atol=0)
+    assert np.allclose(back[hit], rz[hit], rtol=2e-3, atol=0)
+    assert (np.abs(back[hit] - rz[hit]) == 0).mean() > 0.4
