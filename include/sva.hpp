@@ -396,4 +396,98 @@ inline std::vector<double> fuseDepth(Engine& eng, const std::vector<std::vector<
     return depth;
 }
 
+// ---- refinement and 3-D output ----
+// The reference's names and argument meaning; cv::Mat becomes ImageView (u8)
+// or a dense W*H std::vector<double>.  Pixels a routine does not write keep
+// the values of `init` (zeros when omitted) -- the reference leaves them
+// uninitialised.
+
+static_assert(sizeof(Point3d) == 3 * sizeof(double), "Point3d must be three packed doubles");
+
+// shiftPerspectiveWithDisparity -- functions.cpp:50-72.
+inline std::vector<uint8_t> shiftPerspectiveWithDisparity(Engine& eng, const Camera& inputCam,
+                                                          const Camera& outputCam,
+                                                          const ImageView& disparity,
+                                                          const ImageView& image,
+                                                          std::vector<uint8_t> init = {}) {
+    if (disparity.width != image.width || disparity.height != image.height ||
+        disparity.pitch != image.pitch)
+        throw Error(SVA_ERR_INVALID_ARG, "shiftPerspectiveWithDisparity: plane mismatch");
+    init.resize((size_t)image.height * image.pitch, 0);
+    const sva_camera a = inputCam.abi(), b = outputCam.abi();
+    eng.check(sva_shift_perspective(eng.handle(), &a, &b, disparity.data, image.data, image.width,
+                                    image.height, image.pitch, init.data()));
+    return init;
+}
+
+// improveWithDisparity -- functions.cpp:11-48.  `mask` replaces
+// getFaceMask(centerImage) (:13; empty view = every pixel).  strict (default,
+// as the reference): a masked pixel whose window leaves the image throws
+// sva::Error, the analogue of the reference's cv::Exception on that ROI.
+inline std::vector<uint8_t> improveWithDisparity(Engine& eng, const ImageView& disparity,
+                                                 const ImageView& centerImage,
+                                                 const std::vector<ImageView>& images,
+                                                 const std::vector<std::array<Camera, 2>>& cameras,
+                                                 int windowSize,
+                                                 const ImageView& mask = ImageView(),
+                                                 bool strict = true,
+                                                 std::vector<uint8_t> init = {}) {
+    const size_t pitch = centerImage.pitch;
+    auto same = [&](const ImageView& v) {
+        return v.width == centerImage.width && v.height == centerImage.height && v.pitch == pitch;
+    };
+    if (!same(disparity) || (mask.data && !same(mask)) || images.size() != cameras.size())
+        throw Error(SVA_ERR_INVALID_ARG, "improveWithDisparity: plane or pair mismatch");
+    std::vector<const uint8_t*> ptrs;
+    std::vector<sva_camera> cams;
+    for (size_t i = 0; i < images.size(); i++) {
+        if (!same(images[i])) throw Error(SVA_ERR_INVALID_ARG, "improveWithDisparity: image size");
+        ptrs.push_back(images[i].data);
+        cams.push_back(cameras[i][0].abi());
+        cams.push_back(cameras[i][1].abi());
+    }
+    init.resize((size_t)centerImage.height * pitch, 0);
+    eng.check(sva_improve_with_disparity(eng.handle(), disparity.data, centerImage.data,
+                                         ptrs.data(), cams.data(), (int)images.size(),
+                                         centerImage.width, centerImage.height, pitch, mask.data,
+                                         windowSize, strict ? 1 : 0, init.data()));
+    return init;
+}
+
+// shiftPerspective2 -- functions.cpp:74-97 (depth map W*H f64).
+inline std::vector<double> shiftPerspective2(Engine& eng, const Camera& inputCam,
+                                             const Camera& outputCam,
+                                             const std::vector<double>& depthMap, int W, int H,
+                                             std::vector<double> init = {}) {
+    if (depthMap.size() != (size_t)W * H) throw Error(SVA_ERR_INVALID_ARG, "depth map size");
+    init.resize(depthMap.size(), 0.0);
+    const sva_camera a = inputCam.abi(), b = outputCam.abi();
+    eng.check(sva_shift_perspective2(eng.handle(), &a, &b, depthMap.data(), W, H, init.data()));
+    return init;
+}
+
+// Points3DToDepthMap -- functions.cpp:118-132.
+inline std::vector<double> Points3DToDepthMap(Engine& eng, const std::vector<Point3d>& points,
+                                              const Camera& camera, int W, int H,
+                                              std::vector<double> init = {}) {
+    init.resize((size_t)W * H, 0.0);
+    const sva_camera c = camera.abi();
+    eng.check(sva_points_to_depth(eng.handle(), reinterpret_cast<const double*>(points.data()),
+                                  (int64_t)points.size(), &c, W, H, init.data()));
+    return init;
+}
+
+// DepthMapToPoints3D -- functions.cpp:134-146 (column-major order, depth > 0.1).
+inline std::vector<Point3d> DepthMapToPoints3D(Engine& eng, const std::vector<double>& depthMap,
+                                               const Camera& camera, int W, int H) {
+    if (depthMap.size() != (size_t)W * H) throw Error(SVA_ERR_INVALID_ARG, "depth map size");
+    std::vector<Point3d> pts((size_t)W * H);
+    int64_t n = 0;
+    const sva_camera c = camera.abi();
+    eng.check(sva_depth_to_points(eng.handle(), depthMap.data(), W, H, &c,
+                                  reinterpret_cast<double*>(pts.data()), &n));
+    pts.resize((size_t)n);
+    return pts;
+}
+
 }  // namespace sva

@@ -145,6 +145,41 @@ static void gpu_tests() {
                        cams[12].pixel_size, 0xFFFF, &nv);
     const int pc = (H / 2) * W + W / 2;
     CHECK(nv[pc] == 2 && z[pc] == (st.baseline * cams[12].f) / ((double)d0 * cams[12].pixel_size));
+
+    // refinement: img(x) = centre(x - dd - 2) => refined disparity dd + 2 (functions.cpp:11-48)
+    const int dd = 6;
+    std::vector<uint8_t> other(W * H, 0), dispc(W * H, dd), fmask(W * H, 0);
+    for (int y = 0; y < H; y++)
+        for (int x = dd + 2; x < W; x++) other[y * W + x] = imgs[12][y * W + x - dd - 2];
+    for (int y = 40; y < 100; y++)
+        for (int x = 60; x < 130; x++) fmask[y * W + x] = 1;
+    Camera ca(0.05, Point3d{0.05, 0, -0.75}, 1e-4), cb(0.05, Point3d{0, 0, -0.75}, 1e-4);
+    auto refined = improveWithDisparity(eng, ImageView(dispc.data(), W, H), views[12],
+                                        {ImageView(other.data(), W, H)}, {{ca, cb}}, 21,
+                                        ImageView(fmask.data(), W, H));
+    bool allok = true;
+    for (int y = 40; y < 100; y++)
+        for (int x = 60; x < 130; x++) allok = allok && refined[y * W + x] == dd + 2;
+    CHECK(allok && refined[0] == 0);
+    bool threw2 = false;   // full mask: border windows leave the image -> throws like the ROI
+    try {
+        improveWithDisparity(eng, ImageView(dispc.data(), W, H), views[12],
+                             {ImageView(other.data(), W, H)}, {{ca, cb}}, 21);
+    } catch (const Error& e) {
+        threw2 = e.status == SVA_ERR_INVALID_ARG;
+    }
+    CHECK(threw2);
+    // depth -> points -> depth at constant depth 1 on the reference camera
+    std::vector<double> dm((size_t)W * H, 1.0);
+    auto pts = DepthMapToPoints3D(eng, dm, cams[12], W, H);
+    CHECK(pts.size() == (size_t)W * H);
+    auto back = Points3DToDepthMap(eng, pts, cams[12], W, H);
+    CHECK(back[(size_t)(H / 2) * W + W / 2] == 1.0);   // the centre ray is the optical axis
+    auto sh = shiftPerspective2(eng, cams[12], cams[11], dm, W, H);
+    CHECK(sh.size() == dm.size());
+    auto shifted = shiftPerspectiveWithDisparity(eng, cams[12], cams[11], ImageView(dispc.data(), W, H),
+                                                 views[13]);
+    CHECK(shifted[(size_t)10 * W + 10] == imgs[13][(size_t)10 * W + 10 + dd]);
 }
 
 int main(int argc, char** argv) {
