@@ -5,6 +5,8 @@
 // right-census words they touch (PX + D - 1 of them) are staged once in LDS.
 // Each thread produces 16 disparities = one 16-byte store, so a wave writes
 // 1 KiB contiguous.  HBM bytes: 1 B/disparity written + 16 B/pixel read.
+#include <cstdlib>
+
 #include "sva_device.h"
 #include "sva_internal.h"
 
@@ -12,6 +14,8 @@ namespace sva {
 namespace {
 
 constexpr int BLOCK = 256;
+// Out-of-image marker: bit 63 is never set in a census word (bits 0..61).
+constexpr uint64_t kOutside = 1ull << 63;
 constexpr int MAXW = 4096 / 64 + 256;  // LDS words for the smallest D (64): PX=64, +D
 
 // LDS word swizzle.  The D/16 lanes of one pixel read words 16 apart (one per
@@ -87,7 +91,6 @@ __global__ __launch_bounds__(BLOCK) void hamming_cost_kernel(const uint64_t* __r
 // G = 32/NC words per 16 t puts the 32 lanes on 32 distinct bank pairs (D=64,
 // 128; D=192/256 keep a 2-way conflict).  Out-of-image words are staged with
 // bit 63 set, which no census word has (bits 0..61), and read back as 62.
-constexpr uint64_t kOutside = 1ull << 63;
 constexpr int kCost2LdsBytes = 64 * 1024;
 
 template <int NC>
@@ -140,6 +143,98 @@ __global__ __launch_bounds__(BLOCK) void hamming_cost2_kernel(
     }
 }
 
+// Multi-row cost kernel (production).  A workgroup owns PX pixels x ROWS
+// consecutive rows; the next row's right-census words and left word are
+// prefetched into registers while the current row computes, into a second LDS
+// buffer, so HBM latency overlaps compute instead of being paid once per
+// 4 KiB-output workgroup.  One barrier per row: a buffer is rewritten two rows
+// after its last reads and the barrier of the row in between separates them.
+//
+// Lane mapping: 16 consecutive pixels x NC chunks per 16*NC threads (lane
+// l of a 16*NC group: pixel 16g + (l & 15), chunk l >> 4), so a half-wave is
+// 16 pixels x 2 chunks and, for each k, reads words j = lp + 16c + k that are
+// 32 distinct consecutive-or-16-apart words: 32 distinct ds_read_b64 bank
+// pairs with NO swizzle, and each thread's 16 words are consecutive (one base
+// address, immediate offsets).  Out-of-image words carry the bit-63 marker;
+// only workgroups whose word range touches the image border test it.
+// (Measured at 1080p D=128, PMC: the single-row XOR-swizzled kernel spent
+// 7.3M of 16.3M LDS cycles in bank conflicts and ~19 VALU per disparity.)
+constexpr int kCostRows = 16;
+
+template <int NC>
+__global__ __launch_bounds__(256) void hamming_cost_rows_kernel(
+    const uint64_t* __restrict__ cl, const uint64_t* __restrict__ cr, int W, int H, int dmin,
+    int dir, int rows, uint8_t* __restrict__ C) {
+    constexpr int D = NC * 16, NT = (256 / (16 * NC) > 0 ? 256 / (16 * NC) : 1) * 16 * NC;
+    constexpr int PX = NT / NC, NW = PX + D - 1;
+    constexpr int WPT = (NW + NT - 1) / NT;  // staged words per thread
+    __shared__ uint64_t rw[2][NW];
+    const int blocks_per_row = (W + PX - 1) / PX;
+    const int bx = blockIdx.x % blocks_per_row, by = blockIdx.x / blocks_per_row;
+    const int x0 = bx * PX, y0 = by * rows;
+    const int y1 = min(H, y0 + rows);
+    const int t = threadIdx.x;
+    const int g = t / (16 * NC), r = t - g * 16 * NC;
+    const int lp = 16 * g + (r & 15), c = r >> 4;
+    const int x = x0 + lp;
+    const bool active = x < W;
+    // word j <-> column: dir > 0: x0 + dmin + j; dir < 0: x0 + PX - 1 - dmin - j
+    const int first = dir > 0 ? x0 + dmin : x0 + PX - 1 - dmin - (NW - 1);
+    const bool border = first < 0 || first + NW > W;
+    const int j0 = (dir > 0 ? lp : PX - 1 - lp) + 16 * c;
+    uint64_t w[WPT];
+    uint64_t l = 0;
+    auto fetch = [&](int y) {
+#pragma unroll
+        for (int k = 0; k < WPT; k++) {
+            const int j = t + k * NT;
+            const int col = dir > 0 ? x0 + dmin + j : x0 + PX - 1 - dmin - j;
+            w[k] = (j < NW && (unsigned)col < (unsigned)W) ? cr[(size_t)y * W + col] : kOutside;
+        }
+        l = active ? cl[(size_t)y * W + x] : 0;
+    };
+    fetch(y0);
+    for (int y = y0; y < y1; y++) {
+        uint64_t* buf = rw[(y - y0) & 1];
+#pragma unroll
+        for (int k = 0; k < WPT; k++) {
+            const int j = t + k * NT;
+            if (j < NW) buf[j] = w[k];
+        }
+        const uint64_t lc = l;
+        __syncthreads();
+        if (y + 1 < y1) fetch(y + 1);
+        if (active) {
+            const uint64_t* src = buf + j0;
+            unsigned out[4];
+            if (!border) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    unsigned ww = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; b++)
+                        ww |= (unsigned)__popcll(lc ^ src[q * 4 + b]) << (8 * b);
+                    out[q] = ww;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    unsigned ww = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; b++) {
+                        const uint64_t v = lc ^ src[q * 4 + b];
+                        const unsigned cst = (v >> 63) ? 62u : (unsigned)__popcll(v);
+                        ww |= cst << (8 * b);
+                    }
+                    out[q] = ww;
+                }
+            }
+            *(uint4*)(C + ((size_t)y * W + x) * D + 16 * c) =
+                make_uint4(out[0], out[1], out[2], out[3]);
+        }
+    }
+}
+
 }  // namespace
 
 hipError_t launch_cost2(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,
@@ -182,8 +277,24 @@ hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, in
     ScopedKernelTimer t(c, "cost");
     const int px_per_block = BLOCK / (D / 16);
     const int blocks_per_row = (W + px_per_block - 1) / px_per_block;
-    hipLaunchKernelGGL(hamming_cost_kernel, dim3(blocks_per_row * H), dim3(BLOCK), 0, c.stream,
-                       cl, cr, W, H, D, dmin, dir, C);
+    static const int variant = getenv("SVA_COST_VARIANT") ? atoi(getenv("SVA_COST_VARIANT")) : 0;
+    if (variant == 1 || (D != 64 && D != 128 && D != 192 && D != 256)) {  // single-row kernel
+        hipLaunchKernelGGL(hamming_cost_kernel, dim3(blocks_per_row * H), dim3(BLOCK), 0,
+                           c.stream, cl, cr, W, H, D, dmin, dir, C);
+        return hipGetLastError();
+    }
+    const int rows = kCostRows;
+    // threads: 16 pixels x NC chunks per group, as many groups as fit 256
+    const int nc = D / 16, groups = 256 / (16 * nc) > 0 ? 256 / (16 * nc) : 1;
+    const int nt = groups * 16 * nc, px = groups * 16;
+    const int bpr = (W + px - 1) / px;
+    const dim3 grid((unsigned)(bpr * ((H + rows - 1) / rows)));
+    switch (D) {
+        case 64: hipLaunchKernelGGL(hamming_cost_rows_kernel<4>, grid, dim3(nt), 0, c.stream, cl, cr, W, H, dmin, dir, rows, C); break;
+        case 128: hipLaunchKernelGGL(hamming_cost_rows_kernel<8>, grid, dim3(nt), 0, c.stream, cl, cr, W, H, dmin, dir, rows, C); break;
+        case 192: hipLaunchKernelGGL(hamming_cost_rows_kernel<12>, grid, dim3(nt), 0, c.stream, cl, cr, W, H, dmin, dir, rows, C); break;
+        case 256: hipLaunchKernelGGL(hamming_cost_rows_kernel<16>, grid, dim3(nt), 0, c.stream, cl, cr, W, H, dmin, dir, rows, C); break;
+    }
     return hipGetLastError();
 }
 
