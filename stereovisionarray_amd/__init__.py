@@ -17,7 +17,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsva.so")
+# SVA_LIB_PATH: load an alternative build of the same library (kernel-variant
+# experiments under tools/); the default is the in-tree libsva.so.
+LIB_PATH = os.environ.get("SVA_LIB_PATH") or os.path.join(_HERE, "libsva.so")
 
 SVA_OK = 0
 SVA_ERR_INVALID_ARG = 1

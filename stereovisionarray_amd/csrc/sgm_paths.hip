@@ -36,7 +36,48 @@ namespace {
 
 constexpr int PATH_BLOCK = 256;
 constexpr int LINES_PER_BLOCK = PATH_BLOCK / 16;
-constexpr int PF = 8;                        // prefetch depth in steps
+// Prefetch depth in steps, per line kind.  Horizontal lines are the longest
+// (W steps) and few (2H lines): once the vertical/diagonal lines drain they
+// run alone and latency-bound, so they get a deeper ring (their next steps
+// are contiguous bytes, and VGPRs are not what limits occupancy here: the
+// grid has ~3.3 waves per SIMD at 1080p).
+// Measured in-process A/B (tools/ab_paths.py, 1080p D=128, same buffers,
+// alternating builds): PF_H/PF_V 8/8 0.755-0.788 ms; 32/8 0.665; 32/12 0.661;
+// 28/8 0.664; 40/8 0.689 (181 VGPRs -> 2 waves/SIMD); 32/4 0.770.  Part of the
+// gain is the occupancy cap itself: 149 VGPRs -> 3 waves/SIMD, and 8/8 with
+// LDS forcing 3 workgroups/CU is 0.730 vs 0.788 -- fewer concurrent line
+// streams, better DRAM locality.
+// Per disparities-per-lane (D = 16*DPL) overrides: SVA_PF_H<DPL>/SVA_PF_V<DPL>.
+#ifndef SVA_PF_H4
+#define SVA_PF_H4 32
+#endif
+#ifndef SVA_PF_V4
+#define SVA_PF_V4 12
+#endif
+#ifndef SVA_PF_H8
+#define SVA_PF_H8 32
+#endif
+#ifndef SVA_PF_V8
+#define SVA_PF_V8 12
+#endif
+#ifndef SVA_PF_H12
+#define SVA_PF_H12 12
+#endif
+#ifndef SVA_PF_V12
+#define SVA_PF_V12 8
+#endif
+#ifndef SVA_PF_H16
+#define SVA_PF_H16 12
+#endif
+#ifndef SVA_PF_V16
+#define SVA_PF_V16 8
+#endif
+template <int DPL> constexpr int pf_h() {
+    return DPL == 4 ? SVA_PF_H4 : DPL == 8 ? SVA_PF_H8 : DPL == 12 ? SVA_PF_H12 : SVA_PF_H16;
+}
+template <int DPL> constexpr int pf_v() {
+    return DPL == 4 ? SVA_PF_V4 : DPL == 8 ? SVA_PF_V8 : DPL == 12 ? SVA_PF_V12 : SVA_PF_V16;
+}
 constexpr unsigned INF2 = 0x7fff7fffu;       // neighbour beyond d range
 
 struct PathGeom {
@@ -184,7 +225,7 @@ __device__ __forceinline__ void sgm_step(const unsigned (&cw)[DPL / 4], unsigned
     m = row_min_u32(mm.x < mm.y ? mm.x : mm.y);
 }
 
-template <int DPL, bool DIAG, int VAR>
+template <int DPL, bool DIAG, int VAR, int PF>
 __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& g, int rx, int ry,
                                           int line, int k) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
@@ -296,8 +337,9 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
     dir_of(r, rx, ry);
     const rsrc_t rC = make_rsrc(C, g.vol);
     const rsrc_t rL = make_rsrc(L8 + (size_t)r * g.vol, g.vol);
-    if (r >= 4) path_line<DPL, true, VAR>(rC, rL, g, rx, ry, line, k);
-    else path_line<DPL, false, VAR>(rC, rL, g, rx, ry, line, k);
+    if (r >= 4) path_line<DPL, true, VAR, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k);
+    else if (r >= 2) path_line<DPL, false, VAR, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k);
+    else path_line<DPL, false, VAR, pf_h<DPL>()>(rC, rL, g, rx, ry, line, k);
 }
 
 }  // namespace
@@ -315,6 +357,20 @@ hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, i
     g.store_aux = 0;
     if (g.vol >= (size_t)1 << 32) return hipErrorInvalidValue;  // 32-bit buffer offsets
     dim3 grid(2 * g.blk_h + 6 * g.blk_w);
+#ifdef SVA_PATHS_LDS_KB
+    // occupancy experiment: reserve dynamic LDS to cap workgroups per CU
+    {
+        const size_t lds = (size_t)SVA_PATHS_LDS_KB * 1024;
+        switch (D) {
+            case 64: hipLaunchKernelGGL(sgm_paths_kernel<4>, grid, dim3(PATH_BLOCK), lds, c.stream, C, L8, g); break;
+            case 128: hipLaunchKernelGGL(sgm_paths_kernel<8>, grid, dim3(PATH_BLOCK), lds, c.stream, C, L8, g); break;
+            case 192: hipLaunchKernelGGL(sgm_paths_kernel<12>, grid, dim3(PATH_BLOCK), lds, c.stream, C, L8, g); break;
+            case 256: hipLaunchKernelGGL(sgm_paths_kernel<16>, grid, dim3(PATH_BLOCK), lds, c.stream, C, L8, g); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+#endif
 #ifdef SVA_PATHS_ABLATION
     static int var = getenv("SVA_PATHS_VARIANT") ? atoi(getenv("SVA_PATHS_VARIANT")) : 0;
     if (D == 128 && var > 0) {

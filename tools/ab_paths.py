@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""In-process A/B of sgm_paths kernel builds: load several libsva variants
+(ctypes handles side by side), run sva_paths_d on the SAME device C / L
+buffers, alternating variants launch by launch, and report the median
+hipEvent time per variant (run-level effects -- memory placement, clocks --
+hit every variant alike).
+
+usage: ab_paths.py lib1.so lib2.so ... [--W 1920 --H 1080 --D 128 --iters 30]
+"""
+import argparse
+import ctypes as ct
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--W", type=int, default=1920)
+    ap.add_argument("--H", type=int, default=1080)
+    ap.add_argument("--D", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--entry", default="paths", choices=["paths", "sgm"])
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import stereovisionarray_amd as sva   # preloads torch's HIP runtime
+    from stereovisionarray_amd import synth
+
+    W, H, D = a.W, a.H, a.D
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=1)
+    dL, dR = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
+    disp = torch.zeros((H, W), dtype=torch.int16, device=dev)
+    C = torch.zeros((H, W, D), dtype=torch.uint8, device=dev)
+    L8 = torch.zeros((8, H, W, D), dtype=torch.uint8, device=dev)
+    p = sva.default_params(D=D)
+    handles = []
+    for path in a.libs:
+        lib = ct.CDLL(os.path.abspath(path))
+        h = ct.c_void_p()
+        assert lib.sva_create(0, ct.byref(h)) == 0
+        assert lib.sva_set_stream(h, ct.c_void_p(s.cuda_stream)) == 0
+        handles.append((os.path.basename(path), lib, h))
+    # a real cost volume: run the full pipeline once with the first library
+    name0, lib0, h0 = handles[0]
+    assert lib0.sva_disparity_sgm_d(h0, ct.c_void_p(dL.data_ptr()), ct.c_void_p(dR.data_ptr()), W,
+                                    H, ct.c_size_t(W), ct.byref(p), ct.c_void_p(disp.data_ptr()),
+                                    None) == 0
+    C_src = C
+    # build C with the cost stage of lib0 (census via stage calls)
+    cl = torch.zeros((H, W), dtype=torch.int64, device=dev)
+    cr = torch.zeros((H, W), dtype=torch.int64, device=dev)
+    lib0.sva_census_d(h0, ct.c_void_p(dL.data_ptr()), W, H, ct.c_size_t(W), ct.c_void_p(cl.data_ptr()))
+    lib0.sva_census_d(h0, ct.c_void_p(dR.data_ptr()), W, H, ct.c_size_t(W), ct.c_void_p(cr.data_ptr()))
+    lib0.sva_cost_d(h0, ct.c_void_p(cl.data_ptr()), ct.c_void_p(cr.data_ptr()), W, H, ct.byref(p),
+                    ct.c_void_p(C_src.data_ptr()))
+    torch.cuda.synchronize()
+    times = {n: [] for n, _, _ in handles}
+    ref = None
+    for it in range(a.iters + 2):
+        for n, lib, h in handles:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            if a.entry == "paths":
+                st = lib.sva_paths_d(h, ct.c_void_p(C.data_ptr()), W, H, ct.byref(p),
+                                     ct.c_void_p(L8.data_ptr()))
+            else:
+                st = lib.sva_disparity_sgm_d(h, ct.c_void_p(dL.data_ptr()), ct.c_void_p(dR.data_ptr()),
+                                             W, H, ct.c_size_t(W), ct.byref(p),
+                                             ct.c_void_p(disp.data_ptr()), None)
+            e1.record(s)
+            assert st == 0, (n, st)
+            e1.synchronize()
+            if it >= 2:
+                times[n].append(e0.elapsed_time(e1))
+        if a.entry == "paths" and it == 0:
+            # every variant must produce the same volumes
+            outs = []
+            for n, lib, h in handles:
+                lib.sva_paths_d(h, ct.c_void_p(C.data_ptr()), W, H, ct.byref(p),
+                                ct.c_void_p(L8.data_ptr()))
+                torch.cuda.synchronize()
+                outs.append(torch.sum(L8.view(torch.int64)).item())
+            assert len(set(outs)) == 1, outs
+    res = {n: {"median_ms": round(statistics.median(v), 4), "min_ms": round(min(v), 4)}
+           for n, v in times.items()}
+    print(json.dumps({"W": W, "H": H, "D": D, "entry": a.entry, "iters": a.iters,
+                      "variants": res}), flush=True)
+    for n, lib, h in handles:
+        lib.sva_destroy(h)
+
+
+if __name__ == "__main__":
+    main()
