@@ -48,8 +48,11 @@ constexpr int LINES_PER_BLOCK = PATH_BLOCK / 16;
 // LDS forcing 3 workgroups/CU is 0.730 vs 0.788 -- fewer concurrent line
 // streams, better DRAM locality.
 // Per disparities-per-lane (D = 16*DPL) overrides: SVA_PF_H<DPL>/SVA_PF_V<DPL>.
+// Chosen by the same in-process A/B: D=64 (1080p) 40/12 0.372 ms vs 8/8 0.416;
+// D=192 24/8 0.996 vs 12/8 1.154; D=256 (4K) 12/8 stays best (16/8 equal,
+// 20/8 and 12/12 +3 %).
 #ifndef SVA_PF_H4
-#define SVA_PF_H4 32
+#define SVA_PF_H4 40
 #endif
 #ifndef SVA_PF_V4
 #define SVA_PF_V4 12
@@ -61,7 +64,7 @@ constexpr int LINES_PER_BLOCK = PATH_BLOCK / 16;
 #define SVA_PF_V8 12
 #endif
 #ifndef SVA_PF_H12
-#define SVA_PF_H12 12
+#define SVA_PF_H12 24
 #endif
 #ifndef SVA_PF_V12
 #define SVA_PF_V12 8
