@@ -207,6 +207,17 @@ int sva_depth_to_points_d(void* ctx, const double* depth, int width, int height,
 int sva_depth_to_points(void* ctx, const double* depth, int width, int height,
                         const sva_camera* cam, double* points, int64_t* n_points);
 
+/* ------------------------------------------ ingestion --
+ * resize(img, img, Size(), 0.5, 0.5) with the default INTER_LINEAR
+ * (CameraStereoVision.cpp:18): OpenCV 4.2's exact-2x area path -- output
+ * (cvRound(W/2), cvRound(H/2)) (half to even), full 2x2 blocks
+ * (sum + 2) >> 2, partial edge blocks cvRound(sum / count).  u8 planes. */
+int sva_resize_half_size(int width, int height, int* out_width, int* out_height);
+int sva_resize_half_d(void* ctx, const uint8_t* src, int width, int height, size_t pitch,
+                      uint8_t* dst, size_t dst_pitch);
+int sva_resize_half(void* ctx, const uint8_t* src, int width, int height, size_t pitch,
+                    uint8_t* dst, size_t dst_pitch);
+
 /* Multi-pair depth fusion on the root: per
  * pixel the median of baseline_i * f / (disp_i * pixel_size) over the maps
  * with disp_i != invalid and disp_i > 0 (mean of the middle two for an even

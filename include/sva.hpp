@@ -19,7 +19,9 @@
 // bad input); nothing throws across the C-ABI itself.
 #pragma once
 
+#include <algorithm>
 #include <array>
+#include <filesystem>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -488,6 +490,32 @@ inline std::vector<Point3d> DepthMapToPoints3D(Engine& eng, const std::vector<do
                                   reinterpret_cast<double*>(pts.data()), &n));
     pts.resize((size_t)n);
     return pts;
+}
+
+// ---- ingestion ---------------------------------------
+
+// getImagesPathsFromFolder -- functions.cpp:240-250, sorted by file name (the
+// reference's directory_iterator order is unspecified).
+inline std::vector<std::string> getImagesPathsFromFolder(const std::string& folderPath) {
+    std::vector<std::string> filePaths;
+    for (auto& p : std::filesystem::directory_iterator(folderPath))
+        if (p.is_regular_file()) filePaths.push_back(p.path().u8string());
+    std::sort(filePaths.begin(), filePaths.end());
+    return filePaths;
+}
+
+// resize(img, img, Size(), 0.5, 0.5) -- CameraStereoVision.cpp:18 (INTER_LINEAR
+// at exactly 2x = OpenCV's area path), on the GPU.  Returns a dense image of
+// *outW x *outH.
+inline std::vector<uint8_t> resizeHalf(Engine& eng, const ImageView& img, int* outW, int* outH) {
+    int dw = 0, dh = 0;
+    eng.check(sva_resize_half_size(img.width, img.height, &dw, &dh));
+    std::vector<uint8_t> out((size_t)dw * dh);
+    eng.check(sva_resize_half(eng.handle(), img.data, img.width, img.height, img.pitch,
+                              out.data(), (size_t)(dw > 0 ? dw : 1)));
+    if (outW) *outW = dw;
+    if (outH) *outH = dh;
+    return out;
 }
 
 }  // namespace sva

@@ -67,6 +67,8 @@ def _load():
         "svo_shift_perspective2": (None, [P(OCamera), P(OCamera), vp, i32, i32, vp]),
         "svo_points_to_depth": (None, [vp, ct.c_int64, P(OCamera), i32, i32, vp]),
         "svo_depth_to_points": (ct.c_int64, [vp, i32, i32, P(OCamera), vp]),
+        "svo_resize_half_size": (None, [i32, i32, P(i32), P(i32)]),
+        "svo_resize_half": (None, [vp, i32, i32, ct.c_ssize_t, vp, ct.c_ssize_t]),
     }
     for n, (r, a) in sig.items():
         f = getattr(lib, n)
@@ -294,3 +296,13 @@ def depth_to_points(depth, cam):
     pts = np.zeros((W * H, 3), np.float64)
     n = lib.svo_depth_to_points(_p(depth), W, H, ct.byref(cam), _p(pts))
     return pts[:n].copy()
+
+
+def resize_half(img):
+    img = _c(img, np.uint8)
+    H, W = img.shape
+    dw, dh = ct.c_int(0), ct.c_int(0)
+    lib.svo_resize_half_size(W, H, ct.byref(dw), ct.byref(dh))
+    out = np.zeros((dh.value, dw.value), np.uint8)
+    lib.svo_resize_half(_p(img), W, H, W, _p(out), max(1, dw.value))
+    return out

@@ -169,3 +169,40 @@ int64_t svo_depth_to_points(const double* depth, int W, int H, const svo_camera*
         }
     return n;
 }
+
+/* ---- ingestion: resize(img, img, Size(), 0.5, 0.5) -----
+ * CameraStereoVision.cpp:18 with the default INTER_LINEAR.  OpenCV 4.2 routes
+ * an exact 2x INTER_LINEAR reduction to its fast INTER_AREA path (third-party,
+ * absent here: parity unpinned; restated from its published algorithm):
+ *   dsize = (cvRound(W * 0.5), cvRound(H * 0.5))      (round half to even)
+ *   full 2x2 block:    dst = (s00 + s01 + s10 + s11 + 2) >> 2
+ *   partial block (the last row/column when cvRound rounded up):
+ *                      dst = cvRound(sum / count) over the in-image pixels   */
+static int cv_round_half_even(double v) {
+    double r = floor(v + 0.5);
+    if (r - v == 0.5 && fmod(r, 2.0) != 0.0) r -= 1.0;   /* exact .5: to even */
+    return (int)r;
+}
+
+void svo_resize_half_size(int W, int H, int* dw, int* dh) {
+    *dw = cv_round_half_even(W * 0.5);
+    *dh = cv_round_half_even(H * 0.5);
+}
+
+void svo_resize_half(const uint8_t* src, int W, int H, ptrdiff_t pitch, uint8_t* dst,
+                     ptrdiff_t dpitch) {
+    int dw, dh;
+    svo_resize_half_size(W, H, &dw, &dh);
+    for (int y = 0; y < dh; y++)
+        for (int x = 0; x < dw; x++) {
+            int sx = 2 * x, sy = 2 * y, sum = 0, cnt = 0;
+            for (int v = 0; v < 2; v++)
+                for (int u = 0; u < 2; u++)
+                    if (sx + u < W && sy + v < H) {
+                        sum += src[(size_t)(sy + v) * pitch + sx + u];
+                        cnt++;
+                    }
+            dst[(size_t)y * dpitch + x] =
+                cnt == 4 ? (uint8_t)((sum + 2) >> 2) : (uint8_t)cv_round_half_even((double)sum / cnt);
+        }
+}

@@ -169,6 +169,12 @@ void svo_points_to_depth(const double* pts, int64_t n, const svo_camera* cam, in
 int64_t svo_depth_to_points(const double* depth, int W, int H, const svo_camera* cam,
                             double* pts);
 
+/* Ingestion: resize(..., 0.5, 0.5) INTER_LINEAR as OpenCV
+ * 4.2's exact-2x area path (refine_oracle.c; parity unpinned, OpenCV absent). */
+void svo_resize_half_size(int W, int H, int* dw, int* dh);
+void svo_resize_half(const uint8_t* src, int W, int H, ptrdiff_t pitch, uint8_t* dst,
+                     ptrdiff_t dpitch);
+
 #ifdef __cplusplus
 }
 #endif

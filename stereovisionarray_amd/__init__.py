@@ -40,7 +40,8 @@ EXPORTED = [
     "sva_shift_perspective_d", "sva_shift_perspective", "sva_improve_with_disparity_d",
     "sva_improve_with_disparity", "sva_shift_perspective2_d", "sva_shift_perspective2",
     "sva_points_to_depth_d", "sva_points_to_depth", "sva_depth_to_points_d",
-    "sva_depth_to_points", "sva_batch_sgm",
+    "sva_depth_to_points", "sva_resize_half_size", "sva_resize_half_d", "sva_resize_half",
+    "sva_batch_sgm",
 ]
 
 
@@ -147,6 +148,9 @@ def _load() -> ct.CDLL:
         "sva_points_to_depth": (i32, [vp, vp, ct.c_int64, P(Camera), i32, i32, vp]),
         "sva_depth_to_points_d": (i32, [vp, vp, i32, i32, P(Camera), vp, P(ct.c_int64)]),
         "sva_depth_to_points": (i32, [vp, vp, i32, i32, P(Camera), vp, P(ct.c_int64)]),
+        "sva_resize_half_size": (i32, [i32, i32, P(i32), P(i32)]),
+        "sva_resize_half_d": (i32, [vp, vp, i32, i32, sz, vp, sz]),
+        "sva_resize_half": (i32, [vp, vp, i32, i32, sz, vp, sz]),
         "sva_batch_sgm": (i32, [P(vp), i32, P(PairJob), i32, P(SgmParams)]),
     }
     for name, (res, args) in sig.items():
@@ -165,6 +169,14 @@ def default_params(**kw) -> SgmParams:
     for k, v in kw.items():
         setattr(p, k, v)
     return p
+
+
+def resize_half_size(W: int, H: int):
+    """Output size of the ingestion resize: (cvRound(W/2), cvRound(H/2))."""
+    dw, dh = ct.c_int(0), ct.c_int(0)
+    if lib.sva_resize_half_size(W, H, ct.byref(dw), ct.byref(dh)) != 0:
+        raise ValueError("bad size")
+    return dw.value, dh.value
 
 
 def device_count() -> int:
@@ -364,6 +376,18 @@ class Context:
         self._chk(lib.sva_depth_to_points_d(self.h, _ptr(depth), W, H, ct.byref(cam),
                                             _ptr(points), ct.byref(n)))
         return n.value
+
+    # -- ingestion
+    def resize_half(self, img):
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        H, W = img.shape
+        dw, dh = resize_half_size(W, H)
+        out = np.zeros((dh, dw), np.uint8)
+        self._chk(lib.sva_resize_half(self.h, _ptr(img), W, H, W, _ptr(out), max(1, dw)))
+        return out
+
+    def resize_half_d(self, src, W, H, pitch, dst, dst_pitch):
+        self._chk(lib.sva_resize_half_d(self.h, _ptr(src), W, H, pitch, _ptr(dst), dst_pitch))
 
     def fuse_depth(self, disps: np.ndarray, baselines, f, pixel_size, invalid=0xFFFF):
         d = np.ascontiguousarray(disps, dtype=np.uint16)

@@ -875,6 +875,48 @@ int sva_depth_to_points(void* ctx, const double* depth, int W, int H, const sva_
     return SVA_OK;
 }
 
+// ---------------------------------------------------- ingestion (§8f 4) --
+int sva_resize_half_size(int W, int H, int* out_w, int* out_h) {
+    if (W < 0 || H < 0 || !out_w || !out_h) return SVA_ERR_INVALID_ARG;
+    resize_half_size(W, H, out_w, out_h);
+    return SVA_OK;
+}
+
+int sva_resize_half_d(void* ctx, const uint8_t* src, int W, int H, size_t pitch, uint8_t* dst,
+                      size_t dst_pitch) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s, dw, dh;
+    if ((s = check_planes(c, W, H, pitch))) return s;
+    resize_half_size(W, H, &dw, &dh);
+    if (!src || (!dst && dw > 0 && dh > 0) || dst_pitch < (size_t)dw)
+        return fail(c, SVA_ERR_INVALID_ARG, "bad resize argument");
+    SVA_HIP(c, launch_resize_half(*c, src, W, H, pitch, dst, dst_pitch), "resize launch");
+    return SVA_OK;
+}
+
+int sva_resize_half(void* ctx, const uint8_t* src, int W, int H, size_t pitch, uint8_t* dst,
+                    size_t dst_pitch) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s, dw, dh;
+    if ((s = check_planes(c, W, H, pitch))) return s;
+    resize_half_size(W, H, &dw, &dh);
+    if (!src || (!dst && dw > 0 && dh > 0) || dst_pitch < (size_t)dw)
+        return fail(c, SVA_ERR_INVALID_ARG, "bad resize argument");
+    if (dw == 0 || dh == 0) return SVA_OK;
+    const size_t sb = (size_t)H * pitch, db = (size_t)dh * dst_pitch;
+    SVA_HIP(c, c->in_a.ensure(sb), "staging");
+    SVA_HIP(c, c->out_a.ensure(db), "staging");
+    hipStream_t st = c->stream;
+    SVA_HIP(c, hipMemcpyAsync(c->in_a.ptr, src, sb, hipMemcpyHostToDevice, st), "upload");
+    SVA_HIP(c, launch_resize_half(*c, (uint8_t*)c->in_a.ptr, W, H, pitch, (uint8_t*)c->out_a.ptr,
+                                  dst_pitch), "resize launch");
+    SVA_HIP(c, hipMemcpyAsync(dst, c->out_a.ptr, db, hipMemcpyDeviceToHost, st), "download");
+    SVA_HIP(c, hipStreamSynchronize(st), "sync");
+    return SVA_OK;
+}
+
 // ---------------------------------------------------------------- batch --
 int sva_batch_sgm(void** ctxs, int n_ctx, const sva_pair_job* jobs, int n_jobs,
                   const sva_sgm_params* p) {

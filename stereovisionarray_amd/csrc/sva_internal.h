@@ -130,6 +130,10 @@ size_t d2p_units(int W, int H);
 hipError_t launch_depth_to_points(Ctx& c, const double* depth, int W, int H,
                                   const sva_camera& cam, unsigned* counts, long long* total,
                                   double* pts);
+// ingest.hip
+void resize_half_size(int W, int H, int* dw, int* dh);
+hipError_t launch_resize_half(Ctx& c, const uint8_t* src, int W, int H, size_t pitch,
+                              uint8_t* dst, size_t dpitch);
 hipError_t launch_disp_to_depth(Ctx& c, const uint8_t* disp, int n, double cam_distance,
                                 double f, double pixel_size, double* depth);
 

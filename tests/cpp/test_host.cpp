@@ -3,6 +3,7 @@
 //   ./test_host gpu   -- computeDisparity / computeDisparitySGM through the C-ABI
 #include <cstdio>
 #include <cstring>
+#include <fstream>
 #include <random>
 
 #include "sva.hpp"
@@ -76,6 +77,15 @@ static void cpu_tests() {
     CHECK(s7.dir == 0 && s7.dir_y == 1 && s7.k == 1);
     PairStep s3 = pairStep(rc[12], rc[3]);     // grid offset (1,-2)
     CHECK(s3.dir == -1 && s3.dir_y == 2 && s3.k == 2 && std::fabs(s3.baseline - 0.1) < 1e-12);
+    // getImagesPathsFromFolder: sorted listing of regular files
+    auto dir = std::filesystem::temp_directory_path() / "sva_host_test_listing";
+    std::filesystem::remove_all(dir);
+    std::filesystem::create_directories(dir / "sub");
+    for (const char* n : {"b.png", "a.png", "10.png"}) std::ofstream(dir / n) << "x";
+    auto files = getImagesPathsFromFolder(dir.string());
+    CHECK(files.size() == 3 && files[0] == (dir / "10.png").string() &&
+          files[2] == (dir / "b.png").string());
+    std::filesystem::remove_all(dir);
     PairStep s14 = pairStep(rc[12], rc[14]);   // (2,0): reduced to a unit step
     CHECK(s14.dir == -1 && s14.dir_y == 0 && s14.k == 2);
 }
@@ -180,6 +190,12 @@ static void gpu_tests() {
     auto shifted = shiftPerspectiveWithDisparity(eng, cams[12], cams[11], ImageView(dispc.data(), W, H),
                                                  views[13]);
     CHECK(shifted[(size_t)10 * W + 10] == imgs[13][(size_t)10 * W + 10 + dd]);
+    // ingestion resize (CameraStereoVision.cpp:18)
+    int hw = 0, hh = 0;
+    auto half = resizeHalf(eng, views[0], &hw, &hh);
+    CHECK(hw == W / 2 && hh == H / 2 && half.size() == (size_t)hw * hh);
+    const int s4 = imgs[0][0] + imgs[0][1] + imgs[0][W] + imgs[0][W + 1];
+    CHECK(half[0] == (uint8_t)((s4 + 2) >> 2));
 }
 
 int main(int argc, char** argv) {

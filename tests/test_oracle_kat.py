@@ -382,3 +382,20 @@ def test_points_depth_kat(oracle):
     r = 1 / np.sqrt(2.0)
     assert p.shape == (2, 3)
     assert np.allclose(p[0], [0, -r, r], atol=0, rtol=1e-15) and p[1].tolist() == [0, 0, 2]
+
+
+def test_resize_half_kat(oracle):
+    """CameraStereoVision.cpp:18 (OpenCV exact-2x area path): full blocks
+    (sum+2)>>2; partial edge blocks cvRound(sum/count), half to even; output
+    (cvRound(W/2), cvRound(H/2))."""
+    a = np.array([[1, 2, 3, 4, 5], [5, 6, 7, 8, 9], [10, 11, 12, 13, 14]], np.uint8)
+    # W=5 -> cvRound(2.5) = 2, H=3 -> cvRound(1.5) = 2: the last row is partial
+    # (10+11)/2 = 10.5 -> 10 (even), (12+13)/2 = 12.5 -> 12
+    assert oracle.resize_half(a).tolist() == [[4, 6], [10, 12]]
+    b = np.array([[0, 1, 2], [3, 4, 6]], np.uint8)   # W=3 -> 2 columns, last partial
+    # (0+1+3+4+2)>>2 = 2; (2+6)/2 = 4
+    assert oracle.resize_half(b).tolist() == [[2, 4]]
+    c = np.array([[1, 2, 3, 4, 5, 6, 7]], np.uint8)   # H=1 -> cvRound(0.5) = 0 rows
+    assert oracle.resize_half(c).shape == (0, 4)
+    d = np.array([[255, 254], [255, 254]], np.uint8)  # (1018+2)>>2 = 255 (no overflow)
+    assert oracle.resize_half(d).tolist() == [[255]]
