@@ -62,6 +62,11 @@ def parse():
     ap.add_argument("--pairs-per-rank", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=1)
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="gather each step's maps synchronously on the compute stream")
+    ap.add_argument("--rehearse-overlap", action="store_true",
+                    help="N=1 only: run the overlapped-gather stream logic with a device copy "
+                         "standing in for the RCCL gather (RCCL refuses 2 ranks on 1 GPU)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (real runs); gloo = rehearsal with ranks "
                          "sharing one GPU, maps gathered through host memory")
@@ -331,23 +336,56 @@ def main():
         L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=seed0 + u)
         lefts.append(torch.from_numpy(L).to(dev))
         rights.append(torch.from_numpy(R).to(dev))
-    disp = torch.zeros((P, H, W), dtype=torch.int16, device=dev)
+    # Two map buffers: step i computes into buffer i%2 on the compute stream
+    # while the gather of step i-1 (buffer (i-1)%2) runs on a comm stream.
+    overlap = (world > 1 and a.dist_backend == "nccl" and not a.no_overlap) or \
+        (world == 1 and a.rehearse_overlap)
+    nbuf = 2 if overlap else 1
+    disps = [torch.zeros((P, H, W), dtype=torch.int16, device=dev) for _ in range(nbuf)]
     sub = torch.zeros((P, H, W), dtype=torch.float32, device=dev)
+    comm = torch.cuda.Stream(dev) if nbuf == 2 else None
+    gathered = [None] * nbuf            # buffer -> event recorded after its gather
+    it = [0]
+    rehearsal = [torch.zeros((P, H, W), dtype=torch.int16, device=dev)] if world == 1 else None
+
+    def gather(disp):
+        if world > 1:
+            sdist.gather_maps(disp, n_units, dst=0)
+        else:                            # --rehearse-overlap stand-in for the RCCL gather
+            rehearsal[0].copy_(disp)
 
     def step():
+        b = it[0] % nbuf
+        it[0] += 1
+        disp = disps[b]
+        if gathered[b] is not None:      # the previous gather of this buffer is done
+            stream.wait_event(gathered[b])
         for j in range(P):
             ctx.disparity_sgm_d(lefts[j].data_ptr(), rights[j].data_ptr(), W, H, W, params,
                                 disp[j].data_ptr(), sub[j].data_ptr())
-        if world > 1:   # the path's one exchange: disparity maps -> rank 0 (RCCL)
-            if a.dist_backend == "nccl":
-                sdist.gather_maps(disp, n_units, dst=0)
-            else:
+        if world > 1 or comm is not None:   # the path's one exchange: maps -> rank 0 (RCCL)
+            if a.dist_backend == "gloo" and world > 1:
                 sdist.gather_maps(disp.cpu(), n_units, dst=0)
+            elif comm is None:
+                gather(disp)
+            else:
+                done = torch.cuda.Event()
+                done.record(stream)
+                with torch.cuda.stream(comm):
+                    comm.wait_event(done)
+                    disp.record_stream(comm)
+                    gather(disp)
+                    ev = torch.cuda.Event()
+                    ev.record(comm)
+                    gathered[b] = ev
 
     elapsed = timed(a, step, world, dev, ctx)
     kernels = kernel_table(ctx)
     # sanity: the result is a real disparity map (exact on the stripe interiors)
-    d0 = disp[0].cpu().numpy().view(np.uint16)
+    d0 = disps[0][0].cpu().numpy().view(np.uint16)
+    if rehearsal is not None and comm is not None:
+        last = disps[(it[0] - 1) % nbuf]
+        assert torch.equal(rehearsal[0], last), "overlapped gather copied the wrong buffer"
     assert d0.max() < D, "disparity out of range"
 
     units = world * P * a.steps
@@ -372,7 +410,8 @@ def main():
         "config": {"workload": f"{W}x{H} D={D} Mode S SGM (census 9x7, Hamming, 8 paths, "
                                f"WTA+subpixel), {P} pair(s)/rank",
                    "W": W, "H": H, "D": D, "P1": 10, "P2": 120,
-                   "parallelism": f"pairs sharded over {world} rank(s), RCCL gather to rank 0"},
+                   "parallelism": f"pairs sharded over {world} rank(s), RCCL gather to rank 0"
+                                  + (" overlapped with the next step" if nbuf == 2 else "")},
         "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
         "roofline": roofline,
         "cpu_baseline": None,
