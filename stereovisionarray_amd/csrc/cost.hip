@@ -17,11 +17,16 @@ constexpr int BLOCK = 256;
 
 // Cost bytes are stored non-temporally: the 8 path directions re-read C long
 // after it is written and it does not fit the caches anyway (265 MB at 1080p
-// D=128), so write-allocating it only makes sgm_paths pay the dirty-line
-// write-backs.  In-process A/B, full frame 1080p D=128: 1.176 -> 1.132 ms.
+// D=128).  Measured effect: none beyond noise -- an in-process A/B with each
+// build listed twice gave temporal 1.155/1.172 ms vs nt 1.169/1.142 ms per
+// full frame (a first, single-listing A/B had suggested -3.8 %).
 __device__ __forceinline__ void store_cost_nt(uint8_t* p, const unsigned (&o)[4]) {
+#ifdef SVA_COST_TEMPORAL   // A/B switch
+    *(uint4*)p = make_uint4(o[0], o[1], o[2], o[3]);
+#else
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store((v4u){o[0], o[1], o[2], o[3]}, (v4u*)p);
+#endif
 }
 
 // Out-of-image marker: bit 63 is never set in a census word (bits 0..61).

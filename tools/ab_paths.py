@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""In-process A/B of sgm_paths kernel builds: load several libsva variants
+"""In-process A/B of kernel builds (list a build twice to see the noise
+floor: positions in the alternation differ by up to +-2 %): load several libsva variants
 (ctypes handles side by side), run sva_paths_d on the SAME device C / L
 buffers, alternating variants launch by launch, and report the median
 hipEvent time per variant (run-level effects -- memory placement, clocks --
