@@ -73,6 +73,22 @@ def parse():
     return ap.parse_args()
 
 
+def host_cpu():
+    """CPU model and the thread budget this job may use."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    budget = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(nproc, 16)
+    return model, nproc, budget
+
+
 def cpu_baseline(W, H, D, threads):
     """Oracle ('port') timing on this host: the same frame the GPU computes."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -82,13 +98,15 @@ def cpu_baseline(W, H, D, threads):
     t0 = time.perf_counter()
     pyoracle.sgm(L, R, D, 0, -1, 10, 120, subpixel=True, threads=threads)
     dt = time.perf_counter() - t0
+    model, nproc, _ = host_cpu()
     return {
         "value": round(W * H * D / dt / 1e6, 3),
         "unit": "Mdisp/s",
         "cores": threads,
         "kind": "port",
         "sample": f"oracle/sgm_oracle.c svo_sgm, one full {W}x{H} D={D} frame "
-                  f"(census+cost+8 paths+WTA+subpixel), {threads} thread(s), {dt:.2f} s",
+                  f"(census+cost+8 paths+WTA+subpixel), {threads} thread(s), {dt:.2f} s; "
+                  f"host {model}, nproc {nproc}",
     }
 
 
@@ -418,6 +436,9 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(W, H, D, a.cpu_threads)
+        _, _, budget = host_cpu()
+        if budget > 1:   # the oracle at all (allowed) cores as well
+            out["cpu_baseline_all_cores"] = cpu_baseline(W, H, D, budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
