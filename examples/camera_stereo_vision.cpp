@@ -7,7 +7,7 @@
 // No OpenCV here: images are synthetic (one texture seen by every camera
 // through a fronto-parallel plane at depth Z, so the true disparity is known)
 // and nothing is shown on screen.  Build:
-//   g++ -std=c++17 -O2 -I include examples/camera_stereo_vision.cpp \
+//   g++ -std=c++17 -O2 -I include examples/camera_stereo_vision.cpp
 //       -L stereovisionarray_amd -lsva -Wl,-rpath,$PWD/stereovisionarray_amd
 // Run: ./camera_stereo_vision [width height]   (default 640 480)
 #include <chrono>
@@ -33,7 +33,7 @@ int main(int argc, char** argv) {
     // scene point seen at pixel q of camera 12 appears shifted by
     // -(grid offset) * d0 pixels in a neighbour, d0 = pitch * f / (Z * ps).
     // Z inside the reference's ray interval t in [0.5, 1] (:61-64), so Mode R
-    // can find it; d0 < 64 so Mode S with D = 64 can too.
+    // can find it; Mode S gets the smallest built D above d0.
     const int d0 = (int)std::lround(0.05 * f / (0.7 * pixelSize));
     const double Z = 0.05 * f / (d0 * pixelSize);   // the plane depth d0 encodes
     std::mt19937 rng(1234);
@@ -76,7 +76,7 @@ int main(int argc, char** argv) {
     // north_star Mode S on the same pair (12 -> 11: match at x + d)
     sva_sgm_params p;
     sva_sgm_params_default(&p);
-    p.D = 64;
+    p.D = d0 < 64 ? 64 : d0 < 128 ? 128 : d0 < 192 ? 192 : 256;
     p.dir = +1;
     t0 = std::chrono::steady_clock::now();
     auto ds = computeDisparitySGM(engine, images[12], images[11], p);
@@ -84,8 +84,8 @@ int main(int argc, char** argv) {
     long sexact = 0, sn = 0;
     for (int y = 8; y < H - 8; y++)
         for (int x = 8; x < W - 8 - d0; x++, sn++) sexact += ds[(size_t)y * W + x] == d0;
-    std::printf("Mode S (census/SGM, D=64): %.2f ms incl. host copies, %.1f %% of the interior "
-                "at %d\n", t_sgm, 100.0 * sexact / sn, d0);
+    std::printf("Mode S (census/SGM, D=%d): %.2f ms incl. host copies, %.1f %% of the interior "
+                "at %d\n", p.D, t_sgm, 100.0 * sexact / sn, d0);
 
     // TO_CENTER_SMALL: 8 pairs on their own baseline steps, median-fused depth
     auto around = getCameraPairs(cameras, TO_CENTER_SMALL);
