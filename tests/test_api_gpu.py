@@ -1,0 +1,118 @@
+"""C-ABI entry points not covered by the stage tests: the multi-context batch
+(sva_batch_sgm), device (_d) forms of the refinement / 3-D
+routines against their host forms, Mode R on device buffers, workspace
+reservation, the kernel timer and error reporting."""
+import ctypes as ct
+
+import numpy as np
+import pytest
+import torch
+
+from stereovisionarray_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a, d):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(d)
+
+
+def sync(ctx):
+    ctx.synchronize()
+    torch.cuda.synchronize()
+
+
+def test_batch_sgm_matches_single_calls(ctx, sva):
+    """Pair j runs on context j mod N, one host thread per context; results
+    equal one-by-one calls (two contexts on the same device here)."""
+    ctx2 = sva.Context(0)
+    try:
+        pairs = [synth.stereo_pair(72 + 8 * i, 130 - 4 * i, 64, 0, -1, seed=i)[:2] for i in range(5)]
+        p = sva.default_params(D=64, subpixel=1)
+        outs = sva.batch_sgm([ctx, ctx2], pairs, p)
+        for (L, R), (d, s) in zip(pairs, outs):
+            ed, es = ctx.disparity_sgm(L, R, p)
+            assert np.array_equal(d, ed) and np.array_equal(s, es)
+        with pytest.raises(sva.SvaError):
+            sva.batch_sgm([ctx, ctx2], pairs[:1], sva.default_params(D=50))
+    finally:
+        ctx2.close()
+
+
+def test_refine_device_forms_match_host(ctx, sva, torch_dev):
+    W, H = 97, 61
+    cams = synth.reference_array(0.036 / W)
+    ci, co = sva.Camera.make(*cams[12]), sva.Camera.make(*cams[6])
+    rng = np.random.default_rng(4)
+    disp = rng.integers(0, 30, size=(H, W)).astype(np.uint8)
+    img = synth.texture(H, W, 4)
+    host = ctx.shift_perspective(ci, co, disp, img)
+    out = torch.zeros((H, W), dtype=torch.uint8, device=torch_dev)
+    dd, di = dev(disp, torch_dev), dev(img, torch_dev)
+    ctx._chk(sva.lib.sva_shift_perspective_d(ctx.h, ct.byref(ci), ct.byref(co),
+                                             sva._ptr(dd.data_ptr()), sva._ptr(di.data_ptr()),
+                                             W, H, W, sva._ptr(out.data_ptr())))
+    sync(ctx)
+    assert np.array_equal(out.cpu().numpy(), host)
+
+    depth = rng.uniform(0.3, 2.0, size=(H, W))
+    host2 = ctx.shift_perspective2(ci, co, depth)
+    dz = dev(depth, torch_dev)
+    out2 = torch.zeros((H, W), dtype=torch.float64, device=torch_dev)
+    ctx._chk(sva.lib.sva_shift_perspective2_d(ctx.h, ct.byref(ci), ct.byref(co),
+                                              sva._ptr(dz.data_ptr()), W, H,
+                                              sva._ptr(out2.data_ptr())))
+    sync(ctx)
+    assert np.array_equal(out2.cpu().numpy(), host2)
+
+    pts_host = ctx.depth_to_points(depth, ci)
+    pts = torch.zeros((W * H, 3), dtype=torch.float64, device=torch_dev)
+    n = ctx.depth_to_points_d(dz.data_ptr(), W, H, ci, pts.data_ptr())
+    assert n == pts_host.shape[0]
+    assert np.array_equal(pts[:n].cpu().numpy(), pts_host)
+
+    back_host = ctx.points_to_depth(pts_host, ci, W, H)
+    out3 = torch.zeros((H, W), dtype=torch.float64, device=torch_dev)
+    ctx._chk(sva.lib.sva_points_to_depth_d(ctx.h, sva._ptr(pts.data_ptr()), n, ct.byref(ci), W,
+                                           H, sva._ptr(out3.data_ptr())))
+    sync(ctx)
+    assert np.array_equal(out3.cpu().numpy(), back_host)
+
+
+def test_mode_r_device_matches_host(ctx, sva, torch_dev):
+    W, H, k = 160, 96, 8
+    cams = synth.reference_array(0.036 / W)
+    cr, co = sva.Camera.make(*cams[12]), sva.Camera.make(*cams[13])
+    ref = synth.texture(H, W, 7)
+    oth = np.roll(ref, -9, axis=1)
+    h8, h16, hv = ctx.disparity_ref(ref, oth, cr, co, k=k)
+    d8 = torch.zeros((H, W), dtype=torch.uint8, device=torch_dev)
+    d16 = torch.zeros((H, W), dtype=torch.int16, device=torch_dev)
+    val = torch.zeros((H, W), dtype=torch.uint8, device=torch_dev)
+    dr, do = dev(ref, torch_dev), dev(oth, torch_dev)
+    ctx.disparity_ref_d(dr.data_ptr(), do.data_ptr(), W, H, W, None, cr, co, k, 0.5, 1.0,
+                        d8.data_ptr(), d16.data_ptr(), val.data_ptr())
+    sync(ctx)
+    assert np.array_equal(d8.cpu().numpy(), h8)
+    assert np.array_equal(d16.cpu().numpy().view(np.uint16), h16)
+    assert np.array_equal(val.cpu().numpy(), hv)
+
+
+def test_reserve_timing_and_errors(ctx, sva):
+    ctx.reserve(320, 200, 128)                      # grows workspaces up front
+    L, R, _ = synth.stereo_pair(200, 320, 128, 0, -1, seed=2)
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    ctx.disparity_sgm(L, R, sva.default_params(D=128))
+    ctx.disparity_sgm(L, R, sva.default_params(D=128))
+    ctx.set_timing(False)
+    for name in ("census", "cost", "sgm_paths", "wta"):
+        ms, n = ctx.kernel_time(name)
+        assert n == 2 and ms > 0.0, name
+    assert ctx.kernel_time("no_such_kernel") == (0.0, 0)
+    ctx.reset_timing()
+    assert ctx.kernel_time("sgm_paths") == (0.0, 0)
+    with pytest.raises(sva.SvaError) as e:
+        ctx.disparity_sgm(L, R, sva.default_params(D=48))
+    assert "D in {64,128,192,256}" in str(e.value)
+    assert b"D in" in sva.lib.sva_last_error(ctx.h)
