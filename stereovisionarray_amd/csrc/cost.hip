@@ -174,6 +174,9 @@ __global__ __launch_bounds__(BLOCK) void hamming_cost2_kernel(
 // only workgroups whose word range touches the image border test it.
 // (Measured at 1080p D=128, PMC: the single-row XOR-swizzled kernel spent
 // 7.3M of 16.3M LDS cycles in bank conflicts and ~19 VALU per disparity.)
+// Tried and rejected: 64-pixel workgroups (2-4 passes over the 16-pixel
+// groups, less staging traffic per cost byte) -- cost-only A/B: D=128 -2.5 %,
+// D=64 equal, D=192 +22 %, D=256 (4K) +13 %.
 constexpr int kCostRows = 16;
 
 template <int NC>

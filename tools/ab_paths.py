@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--H", type=int, default=1080)
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--iters", type=int, default=30)
-    ap.add_argument("--entry", default="paths", choices=["paths", "sgm"])
+    ap.add_argument("--entry", default="paths", choices=["paths", "sgm", "cost"])
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -73,6 +73,9 @@ def main():
             if a.entry == "paths":
                 st = lib.sva_paths_d(h, ct.c_void_p(C.data_ptr()), W, H, ct.byref(p),
                                      ct.c_void_p(L8.data_ptr()))
+            elif a.entry == "cost":
+                st = lib.sva_cost_d(h, ct.c_void_p(cl.data_ptr()), ct.c_void_p(cr.data_ptr()), W, H,
+                                    ct.byref(p), ct.c_void_p(C.data_ptr()))
             else:
                 st = lib.sva_disparity_sgm_d(h, ct.c_void_p(dL.data_ptr()), ct.c_void_p(dR.data_ptr()),
                                              W, H, ct.c_size_t(W), ct.byref(p),
@@ -82,6 +85,14 @@ def main():
             e1.synchronize()
             if it >= 2:
                 times[n].append(e0.elapsed_time(e1))
+        if a.entry == "cost" and it == 0:
+            outs = []
+            for n, lib, h in handles:
+                lib.sva_cost_d(h, ct.c_void_p(cl.data_ptr()), ct.c_void_p(cr.data_ptr()), W, H,
+                               ct.byref(p), ct.c_void_p(C.data_ptr()))
+                torch.cuda.synchronize()
+                outs.append(torch.sum(C.view(torch.int64)).item())
+            assert len(set(outs)) == 1, outs
         if a.entry == "paths" and it == 0:
             # every variant must produce the same volumes
             outs = []
