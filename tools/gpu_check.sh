@@ -30,6 +30,10 @@ for step in "$@"; do
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     refine_bench) run refine_bench 600 python tools/bench_refine.py ;;
+    prof4k) run prof4k 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4k -o run --output-format csv -- python3 bench.py --workload 4k_d256 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    pmc4k) run pmc4k_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc4k_fetch -o run --output-format csv -- python3 bench.py --workload 4k_d256 --steps 2 --warmup 1 --no-cpu-baseline
+           run pmc4k_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc4k_write -o run --output-format csv -- python3 bench.py --workload 4k_d256 --steps 2 --warmup 1 --no-cpu-baseline
+           run pmc4k_json 120 python3 tools/pmc_traffic.py gpurun_out/pmc4k_fetch gpurun_out/pmc4k_write 3840 2160 256 gpurun_out/pmc_4k_d256.json ;;
     pmcjson) run pmcjson 120 python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write 1920 1080 128 gpurun_out/pmc_1080p_d128.json ;;
     prof_center8) run prof_center8 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_center8 -o run --output-format csv -- python3 bench.py --workload center8 --steps 5 --warmup 2 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
