@@ -110,6 +110,53 @@ def cpu_baseline(W, H, D, threads):
     }
 
 
+def mode_r_beside(ctx, W, H, rows=24, k=20, reps=3):
+    """The reference's own path (Mode R: Bresenham candidates + 2k x 2k SAD,
+    CameraStereoVision.cpp:44-95), GPU vs its CPU restatement on this host,
+    in candidate SADs per second.  Reference rig pair 12 -> 11, k = 20; the
+    CPU leg runs a bounded sample of `rows` image rows (1 thread)."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle  # CPU baseline leg only
+    import stereovisionarray_amd as sva
+    from stereovisionarray_amd import synth
+    cams = synth.reference_array(0.036 / W)
+    cr, co = sva.Camera.make(*cams[12]), sva.Camera.make(*cams[11])
+    ref = synth.texture(H, W, 5)
+    oth = np.roll(ref, int(round(0.05 * 0.05 / 0.75 / (0.036 / W))), axis=1)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    d_ref, d_oth = torch.from_numpy(ref).to(dev), torch.from_numpy(oth).to(dev)
+    d8 = torch.zeros((H, W), dtype=torch.uint8, device=dev)
+    ends = torch.zeros((H, W, 4), dtype=torch.int32, device=dev)
+    ok = torch.zeros((H, W), dtype=torch.uint8, device=dev)
+    ctx.ref_endpoints_d(W, H, cr, co, k, 0.5, 1.0, ends.data_ptr(), ok.data_ptr())
+    torch.cuda.synchronize()
+    e = ends.cpu().numpy().astype(np.int64)
+    okn = ok.cpu().numpy().astype(bool)
+    n_cand = int((np.maximum(np.abs(e[..., 0] - e[..., 2]), np.abs(e[..., 1] - e[..., 3])) + 1)[okn].sum())
+    run = lambda: ctx.disparity_ref_d(d_ref.data_ptr(), d_oth.data_ptr(), W, H, W, None, cr, co, k,
+                                      0.5, 1.0, d8.data_ptr())
+    run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    gdt = (time.perf_counter() - t0) / reps
+    mask = np.zeros((H, W), np.uint8)
+    mask[H // 2 - rows // 2: H // 2 + rows // 2, :] = 1
+    t0 = time.perf_counter()
+    _, _, _, ncpu = pyoracle.ref_pair(ref, oth, pyoracle.OCamera.make(*cams[12]),
+                                      pyoracle.OCamera.make(*cams[11]), k=k, mask=mask)
+    cdt = time.perf_counter() - t0
+    g, c = n_cand / gdt / 1e6, ncpu / cdt / 1e6
+    return {"unit": "Mcandidate-SADs/s", "gpu": round(g, 1), "gpu_ms_per_frame": round(gdt * 1e3, 3),
+            "cpu": round(c, 3), "cores": 1, "kind": "port",
+            "sample": f"oracle/refpath_oracle.c svo_ref_pair, {W}x{H} pair 12->11 k={k}: "
+                      f"{rows} rows, {ncpu} candidates, {cdt:.2f} s",
+            "gpu_over_cpu": round(g / c, 1)}
+
+
 def load_traffic(workload):
     """HBM bytes per sgm_paths launch from the committed rocprofv3 PMC pass
     (profiles/pmc_<workload>.json, written by tools/pmc_traffic.py), or None."""
@@ -439,6 +486,8 @@ def main():
         _, _, budget = host_cpu()
         if budget > 1:   # the oracle at all (allowed) cores as well
             out["cpu_baseline_all_cores"] = cpu_baseline(W, H, D, budget)
+        # the reference's own CPU path (Mode R) timed beside its GPU port
+        out["mode_r"] = mode_r_beside(ctx, W, H)
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

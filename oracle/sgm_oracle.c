@@ -13,6 +13,11 @@
  */
 #include "sva_oracle.h"
 
+/* Threads for the row-parallel stage loops (census, cost, WTA): 1 except
+ * inside a threaded svo_sgm call (the CPU baseline's all-cores leg).  The
+ * arithmetic is the same either way. */
+static int g_threads = 1;
+
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -21,6 +26,9 @@
 
 /* DESIGN.md §2.1 -- census 9 wide x 7 high. */
 void svo_census(const uint8_t* img, int W, int H, ptrdiff_t pitch, uint64_t* out) {
+    #ifdef _OPENMP
+#pragma omp parallel for num_threads(g_threads) schedule(static)
+#endif
     for (int y = 0; y < H; y++) {
         for (int x = 0; x < W; x++) {
             uint64_t w = 0;
@@ -38,15 +46,14 @@ void svo_census(const uint8_t* img, int W, int H, ptrdiff_t pitch, uint64_t* out
     }
 }
 
-static int popcount64(uint64_t v) {
-    int n = 0;
-    while (v) { v &= v - 1; n++; }
-    return n;
-}
+static int popcount64(uint64_t v) { return __builtin_popcountll(v); }
 
 /* DESIGN.md §2.2 -- Hamming matching cost, D-contiguous u8. */
 void svo_cost(const uint64_t* cl, const uint64_t* cr, int W, int H, int D, int dmin, int dir,
               uint8_t* C) {
+    #ifdef _OPENMP
+#pragma omp parallel for num_threads(g_threads) schedule(static)
+#endif
     for (int y = 0; y < H; y++)
         for (int x = 0; x < W; x++)
             for (int d = 0; d < D; d++) {
@@ -144,6 +151,9 @@ void svo_aggregate(const uint8_t* C, int W, int H, int D, int P1, int P2, uint16
 /* DESIGN.md §2.4 -- first-minimum WTA (mirrors CameraStereoVision.cpp:85)
  * and parabola sub-pixel in f32. */
 void svo_wta(const uint16_t* S, int W, int H, int D, int dmin, uint16_t* disp, float* sub) {
+    #ifdef _OPENMP
+#pragma omp parallel for num_threads(g_threads) schedule(static)
+#endif
     for (size_t p = 0; p < (size_t)W * H; p++) {
         const uint16_t* s = S + p * D;
         int best = 0;
@@ -187,23 +197,29 @@ static void path_line_step(const uint8_t* C, uint8_t* L, int W, int H, int D, in
 
 static void svo_path_threaded(const uint8_t* C, int W, int H, int D, int rx, int ry, int P1,
                               int P2, uint8_t* L, int threads) {
-    if (ry == 0) {
-        /* horizontal: rows independent */
+    /* Lines are independent: every pixel whose predecessor p - r leaves the
+     * image starts one, and one thread walks each line in path order.
+     * Entry pixels: the entry row (ry != 0) and the entry column (rx != 0),
+     * the corner counted once. */
+    const int y0 = ry > 0 ? 0 : H - 1, x0 = rx > 0 ? 0 : W - 1;
+    const int nrow = ry != 0 ? W : 0;
+    const int ncol = rx == 0 ? 0 : (ry != 0 ? H - 1 : H);
 #ifdef _OPENMP
-#pragma omp parallel for num_threads(threads) schedule(static)
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 16)
 #endif
-        for (int y = 0; y < H; y++)
-            for (int xi = 0; xi < W; xi++)
-                path_line_step(C, L, W, H, D, rx > 0 ? xi : W - 1 - xi, y, rx, ry, P1, P2);
-    } else {
-        /* vertical / diagonal: a row depends only on the previous row */
-        for (int yi = 0; yi < H; yi++) {
-            int y = ry > 0 ? yi : H - 1 - yi;
-#ifdef _OPENMP
-#pragma omp parallel for num_threads(threads) schedule(static)
-#endif
-            for (int x = 0; x < W; x++) path_line_step(C, L, W, H, D, x, y, rx, ry, P1, P2);
+    for (int e = 0; e < nrow + ncol; e++) {
+        int x, y;
+        if (e < nrow) {
+            x = e;
+            y = y0;
+        } else {
+            int i = e - nrow;                       /* i-th entry-column pixel */
+            x = x0;
+            if (ry == 0) y = i;
+            else y = ry > 0 ? 1 + i : H - 2 - i;    /* skip the corner on the entry row */
         }
+        for (; x >= 0 && x < W && y >= 0 && y < H; x += rx, y += ry)
+            path_line_step(C, L, W, H, D, x, y, rx, ry, P1, P2);
     }
 }
 
@@ -214,6 +230,7 @@ void svo_sgm(const uint8_t* left, const uint8_t* right, int W, int H, ptrdiff_t 
     uint64_t* cr = (uint64_t*)malloc(np * 8);
     uint8_t* C = (uint8_t*)malloc(n);
     uint16_t* S = (uint16_t*)malloc(n * 2);
+    g_threads = threads > 1 ? threads : 1;
     svo_census(left, W, H, pitch, cl);
     svo_census(right, W, H, pitch, cr);
     svo_cost(cl, cr, W, H, D, dmin, dir, C);
@@ -234,6 +251,7 @@ void svo_sgm(const uint8_t* left, const uint8_t* right, int W, int H, ptrdiff_t 
         svo_aggregate(C, W, H, D, P1, P2, S, 1);
     }
     svo_wta(S, W, H, D, dmin, disp, sub);
+    g_threads = 1;
     free(cl);
     free(cr);
     free(C);
