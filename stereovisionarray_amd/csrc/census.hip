@@ -153,7 +153,11 @@ __global__ __launch_bounds__(TX* TY) void census9x7_rows_kernel(
 
 static hipError_t census_launch(Ctx& c, const uint8_t* a, const uint8_t* b, int W, int H,
                                 size_t pitch, uint64_t* oa, uint64_t* ob, int n) {
+#ifdef SVA_PATHS_ABLATION   // A/B builds only: SVA_CENSUS_VARIANT=1 selects the single-tile kernel
     static const int variant = getenv("SVA_CENSUS_VARIANT") ? atoi(getenv("SVA_CENSUS_VARIANT")) : 0;
+#else
+    constexpr int variant = 0;
+#endif
     if (variant == 1) {   // single-tile kernel
         dim3 grid((W + TX - 1) / TX, (H + TY - 1) / TY, n);
         hipLaunchKernelGGL(census9x7_kernel, grid, dim3(TX, TY), 0, c.stream, a, b, W, H, pitch,

@@ -294,7 +294,11 @@ hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, in
     ScopedKernelTimer t(c, "cost");
     const int px_per_block = BLOCK / (D / 16);
     const int blocks_per_row = (W + px_per_block - 1) / px_per_block;
+#ifdef SVA_PATHS_ABLATION   // A/B builds only: SVA_COST_VARIANT=1 selects the single-row kernel
     static const int variant = getenv("SVA_COST_VARIANT") ? atoi(getenv("SVA_COST_VARIANT")) : 0;
+#else
+    constexpr int variant = 0;
+#endif
     if (variant == 1 || (D != 64 && D != 128 && D != 192 && D != 256)) {  // single-row kernel
         hipLaunchKernelGGL(hamming_cost_kernel, dim3(blocks_per_row * H), dim3(BLOCK), 0,
                            c.stream, cl, cr, W, H, D, dmin, dir, C);

@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B of the census / cost kernel variants (env switches), interleaved.
+# Needs the ablation build: make -C stereovisionarray_amd/csrc EXTRA=-DSVA_PATHS_ABLATION
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
 timeout -k 10 900 python -m pytest tests/test_sgm_gpu.py tests/test_array_gpu.py -q -m gpu -x > gpurun_out/ab_tests.log 2>&1; rc=$?
