@@ -126,22 +126,18 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 
 // sad_row<ND>: sva_device.h
 
+// Per-pixel wave algorithm (one wave per reference pixel, one lane per
+// candidate, v_sad_u8 on v_alignbyte-realigned rows).  Used by
+// ref_match_kernel and as the per-tile fallback of ref_plane_kernel.
 template <int ND>
-__global__ __launch_bounds__(256) void ref_match_kernel(
-    const uint8_t* __restrict__ ref, const uint8_t* __restrict__ other, int W, int H, size_t pitch,
-    const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
-    const uint8_t* __restrict__ valid_in, int k, uint8_t* __restrict__ disp_u8,
-    uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out) {
+__device__ __forceinline__ void match_pixel_wave(const uint8_t* __restrict__ ref,
+                                                 const uint8_t* __restrict__ other, int W,
+                                                 size_t pitch, int x, int y, const int4 e, int k,
+                                                 uint8_t* __restrict__ disp_u8,
+                                                 uint16_t* __restrict__ disp_u16,
+                                                 uint8_t* __restrict__ valid_out) {
     const int lane = threadIdx.x & 63;
-    // one wave per pixel of the loop region [k, W-k) x [k, H-k)
-    const int iw = W - 2 * k;
-    const long long q = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-    if (q >= (long long)iw * (H - 2 * k)) return;
-    const int y = k + (int)(q / iw), x = k + (int)(q % iw);
     const size_t p = (size_t)y * W + x;
-    if (!valid_in[p]) return;
-    if (mask && mask[p] == 0) return;                                 // :53
-    const int4 e = ends[p];
     const Line L = make_line(e.x, e.y, e.z, e.w);                     // :73
     const int nbytes = 2 * k;
     const unsigned lastmask = (nbytes & 3) ? 0xffffu : 0xffffffffu;
@@ -166,6 +162,226 @@ __global__ __launch_bounds__(256) void ref_match_kernel(
     if (lane == 0) {
         int cx, cy;
         line_point(L, (int)(best & 0xffffffffu), cx, cy);
+        const double dx = (double)(cx - x), dy = (double)(cy - y);
+        const int dn = (int)__builtin_sqrt(dx * dx + dy * dy);       // :89
+        disp_u8[p] = (uint8_t)dn;
+        if (disp_u16) disp_u16[p] = (uint16_t)dn;
+        if (valid_out) valid_out[p] = 1;
+    }
+}
+
+template <int ND>
+__global__ __launch_bounds__(256) void ref_match_kernel(
+    const uint8_t* __restrict__ ref, const uint8_t* __restrict__ other, int W, int H, size_t pitch,
+    const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
+    const uint8_t* __restrict__ valid_in, int k, uint8_t* __restrict__ disp_u8,
+    uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out) {
+    // one wave per pixel of the loop region [k, W-k) x [k, H-k)
+    const int iw = W - 2 * k;
+    const long long q = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    if (q >= (long long)iw * (H - 2 * k)) return;
+    const int y = k + (int)(q / iw), x = k + (int)(q % iw);
+    const size_t p = (size_t)y * W + x;
+    if (!valid_in[p]) return;
+    if (mask && mask[p] == 0) return;                                 // :53
+    match_pixel_wave<ND>(ref, other, W, pitch, x, y, ends[p], k, disp_u8, disp_u16, valid_out);
+}
+
+// ---- offset-plane algorithm (same results, far less work) -------------------
+//
+// For a fixed offset delta, AD(q) = |O(q + delta) - R(q)| is shared by every
+// reference pixel, and SAD(p, delta) is the 2k x 2k box sum of AD at p.  A
+// workgroup owns a tile of TW = 64 - 2k columns x PT_ROWS rows of reference
+// pixels, whose window-extended region is exactly 64 columns wide.  It
+//   1. collects the union of its pixels' candidate offsets c_i - p in an LDS
+//      bitmap over their bounding box (neighbouring pixels' offsets nearly
+//      coincide, so this is a thin band even for diagonal pairs);
+//   2. per offset plane: AD bytes of the region into LDS (aligned dword loads
+//      of O realigned with v_alignbyte), column sums sliding down the rows,
+//      row sums sliding along x, and for each pixel a division-free test of
+//      whether delta is on ITS Bresenham line -- candidate i on a low line is
+//      x0 + i with minor offset m = floor((a*i + major - 1) / b), i.e.
+//      t*b <= a*i + major - 1 < (t+1)*b for t = step*(c.minor - minor0) --
+//      keeping min over (SAD << 32 | i): the reference's first minimum
+//      (CameraStereoVision.cpp:85) whatever order the planes are visited in.
+// A tile whose offset box exceeds the bitmap falls back to match_pixel_wave.
+constexpr int PT_ROWS = 32;                  // tile rows
+constexpr int PT_REG_W = 64;                 // region width = TW + 2k
+constexpr int PT_MAXK = 28;                  // TW >= 8
+constexpr int PT_REG_H = PT_ROWS + 2 * PT_MAXK;
+constexpr int PT_CS_W = PT_REG_W + 2;        // padded column-sum rows (bank spread)
+constexpr int PT_MAXBITS = 1 << 16;          // offset bitmap capacity
+
+__device__ __forceinline__ bool on_line(const Line& L, int cx, int cy) {
+    int i, t;
+    if (L.high) { i = cy - L.y0; t = L.step * (cx - L.x0); }
+    else { i = cx - L.x0; t = L.step * (cy - L.y0); }
+    if (i < 0 || i >= L.n) return false;
+    if (L.b == 0) return t == 0;
+    const int num = L.a * i + L.major - 1;
+    return t >= 0 && t * L.b <= num && num < (t + 1) * L.b;
+}
+
+__device__ __forceinline__ int line_index(const Line& L, int cx, int cy) {
+    return L.high ? cy - L.y0 : cx - L.x0;
+}
+
+template <int ND>
+__global__ __launch_bounds__(256) void ref_plane_kernel(
+    const uint8_t* __restrict__ ref, const uint8_t* __restrict__ other, int W, int H, size_t pitch,
+    const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
+    const uint8_t* __restrict__ valid_in, int k, uint8_t* __restrict__ disp_u8,
+    uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out) {
+    __shared__ __attribute__((aligned(16))) uint8_t Rr[PT_REG_H][PT_REG_W];   // read as dwords
+    __shared__ __attribute__((aligned(16))) uint8_t AD[PT_REG_H][PT_REG_W];
+    __shared__ unsigned short CS[PT_ROWS][PT_CS_W];
+    __shared__ unsigned bits[PT_MAXBITS / 32];
+    __shared__ int box[4];                    // dx_lo, dx_hi, dy_lo, dy_hi
+    const int t = threadIdx.x;
+    const int TW = PT_REG_W - 2 * k;
+    const int tx0 = k + blockIdx.x * TW, ty0 = k + blockIdx.y * PT_ROWS;
+    const int rx0 = tx0 - k, ry0 = ty0 - k;   // region origin (image coords)
+    const int RH = PT_ROWS + 2 * k;
+    // pixels of this thread: row r = t / 8, x_l in [seg*PPT, seg*PPT + PPT)
+    const int PPT = (TW + 7) / 8;
+    const int r = t >> 3, xs = (t & 7) * PPT;
+    constexpr int MAXPPT = (PT_REG_W - 2 + 7) / 8;   // k >= 1: TW <= 62
+    Line Ls[MAXPPT];
+    bool ok[MAXPPT];
+    unsigned long long best[MAXPPT];
+    if (t < 4) box[t] = (t & 1) ? -0x7fffffff : 0x7fffffff;
+    for (int i = t; i < RH * PT_REG_W; i += 256) {
+        const int v = i >> 6, u = i & 63;
+        const int gx = rx0 + u, gy = ry0 + v;
+        Rr[v][u] = (gx < W && gy < H) ? ref[(size_t)gy * pitch + gx] : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MAXPPT; j++) {
+        ok[j] = false;
+        best[j] = ~0ull;
+        const int xl = xs + j, x = tx0 + xl, y = ty0 + r;
+        if (j >= PPT || xl >= TW || x >= W - k || y >= H - k) continue;
+        const size_t p = (size_t)y * W + x;
+        if (!valid_in[p] || (mask && mask[p] == 0)) continue;
+        const int4 e = ends[p];
+        ok[j] = true;
+        Ls[j] = make_line(e.x, e.y, e.z, e.w);
+        atomicMin(&box[0], min(e.x, e.z) - x);
+        atomicMax(&box[1], max(e.x, e.z) - x);
+        atomicMin(&box[2], min(e.y, e.w) - y);
+        atomicMax(&box[3], max(e.y, e.w) - y);
+    }
+    __syncthreads();
+    const int dxlo = box[0], dylo = box[2];
+    const int bw = box[1] - box[0] + 1, bh = box[3] - box[2] + 1;
+    if (box[1] < box[0]) return;             // no valid pixel in this tile
+    if ((long long)bw * bh > PT_MAXBITS) {
+        // offset box too large for the bitmap: per-pixel waves for this tile
+        const int wave = t >> 6;
+        for (int pi = wave; pi < TW * PT_ROWS; pi += 4) {
+            const int x = tx0 + pi % TW, y = ty0 + pi / TW;
+            if (x >= W - k || y >= H - k) continue;
+            const size_t p = (size_t)y * W + x;
+            if (!valid_in[p] || (mask && mask[p] == 0)) continue;
+            match_pixel_wave<ND>(ref, other, W, pitch, x, y, ends[p], k, disp_u8, disp_u16,
+                                 valid_out);
+        }
+        return;
+    }
+    const int nwords = (bw * bh + 31) >> 5;
+    for (int i = t; i < nwords; i += 256) bits[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MAXPPT; j++) {
+        if (!ok[j]) continue;
+        const int x = tx0 + xs + j, y = ty0 + r;
+        for (int i = 0; i < Ls[j].n; i++) {
+            int cx, cy;
+            line_point(Ls[j], i, cx, cy);
+            const int b = (cy - y - dylo) * bw + (cx - x - dxlo);
+            atomicOr(&bits[b >> 5], 1u << (b & 31));
+        }
+    }
+    __syncthreads();
+    const int cu = t & 63, cseg = t >> 6;    // column-sum thread: column, 8-row segment
+    for (int wd = 0; wd < nwords; wd++) {
+        unsigned m = bits[wd];               // uniform across the workgroup
+        while (m) {
+            const int bit = __builtin_ctz(m);
+            m &= m - 1;
+            const int b = wd * 32 + bit;
+            const int ddy = dylo + b / bw, ddx = dxlo + b % bw;
+            // (a) AD bytes of the region for this plane
+            for (int i = t; i < RH * 16; i += 256) {
+                const int v = i >> 4, u4 = (i & 15) * 4;
+                const int gx = rx0 + u4 + ddx, gy = ry0 + v + ddy;
+                unsigned o;
+                if (gy >= 0 && gy < H && gx >= 0 && gx + 3 < W) {
+                    const uint8_t* src = other + (size_t)gy * pitch + gx;
+                    const uintptr_t a = (uintptr_t)src;
+                    const unsigned* w = (const unsigned*)(a & ~(uintptr_t)3);
+                    const unsigned sh = (unsigned)(a & 3);
+                    // never read the dword after the one holding the last byte
+                    o = sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
+                } else {
+                    o = 0;
+                    for (int q = 0; q < 4; q++) {
+                        const int x = gx + q;
+                        if (gy >= 0 && gy < H && x >= 0 && x < W)
+                            o |= (unsigned)other[(size_t)gy * pitch + x] << (8 * q);
+                    }
+                }
+                const unsigned rr = *(const unsigned*)&Rr[v][u4];
+                unsigned ad = 0;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int d = (int)((o >> (8 * q)) & 0xff) - (int)((rr >> (8 * q)) & 0xff);
+                    ad |= (unsigned)(d < 0 ? -d : d) << (8 * q);
+                }
+                *(unsigned*)&AD[v][u4] = ad;
+            }
+            __syncthreads();
+            // (b) column sums over 2k rows, 8 output rows per thread
+            {
+                const int r0 = cseg * 8;
+                unsigned sacc = 0;
+                for (int v = 0; v < 2 * k; v++) sacc += AD[r0 + v][cu];
+                CS[r0][cu] = (unsigned short)sacc;
+#pragma unroll
+                for (int rr2 = 1; rr2 < 8; rr2++) {
+                    sacc += AD[r0 + rr2 - 1 + 2 * k][cu];
+                    sacc -= AD[r0 + rr2 - 1][cu];
+                    CS[r0 + rr2][cu] = (unsigned short)sacc;
+                }
+            }
+            __syncthreads();
+            // (c) row sums, membership, first-minimum key.  Column sums read:
+            // CS[r][xl .. xl + 2k - 1] with xl < TW: index <= TW + 2k - 2 = 62.
+            if (xs < TW) {
+                unsigned sad = 0;
+                for (int u = 0; u < 2 * k; u++) sad += CS[r][xs + u];
+#pragma unroll
+                for (int j = 0; j < MAXPPT; j++) {
+                    if (j >= PPT || xs + j >= TW) break;
+                    if (j > 0) sad += (unsigned)CS[r][xs + j - 1 + 2 * k] - CS[r][xs + j - 1];
+                    if (!ok[j]) continue;
+                    const int cx = tx0 + xs + j + ddx, cy = ty0 + r + ddy;
+                    if (!on_line(Ls[j], cx, cy)) continue;
+                    const unsigned long long key =
+                        ((unsigned long long)sad << 32) | (unsigned)line_index(Ls[j], cx, cy);
+                    best[j] = key < best[j] ? key : best[j];
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < MAXPPT; j++) {
+        if (!ok[j]) continue;
+        const int x = tx0 + xs + j, y = ty0 + r;
+        const size_t p = (size_t)y * W + x;
+        int cx, cy;
+        line_point(Ls[j], (int)(best[j] & 0xffffffffu), cx, cy);
         const double dx = (double)(cx - x), dy = (double)(cy - y);
         const int dn = (int)__builtin_sqrt(dx * dx + dy * dy);       // :89
         disp_u8[p] = (uint8_t)dn;
@@ -208,6 +424,25 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
     ScopedKernelTimer t(c, "ref_match");
     const long long npx = (long long)(W - 2 * k) * (H - 2 * k);
     if (npx <= 0) return hipSuccess;
+    if (k <= PT_MAXK) {   // offset-plane algorithm
+        const int tw = PT_REG_W - 2 * k;
+        const dim3 pg((unsigned)((W - 2 * k + tw - 1) / tw), (unsigned)((H - 2 * k + PT_ROWS - 1) / PT_ROWS));
+#define SVA_PLANE_CASE(ND)                                                                     \
+    case ND:                                                                                   \
+        hipLaunchKernelGGL(ref_plane_kernel<ND>, pg, dim3(256), 0, c.stream, ref, other, W, H,  \
+                           pitch, mask, (const int4*)ends, valid_in, k, disp_u8, disp_u16,      \
+                           valid_out);                                                         \
+        break;
+        switch ((k + 1) / 2) {
+            SVA_PLANE_CASE(1) SVA_PLANE_CASE(2) SVA_PLANE_CASE(3) SVA_PLANE_CASE(4)
+            SVA_PLANE_CASE(5) SVA_PLANE_CASE(6) SVA_PLANE_CASE(7) SVA_PLANE_CASE(8)
+            SVA_PLANE_CASE(9) SVA_PLANE_CASE(10) SVA_PLANE_CASE(11) SVA_PLANE_CASE(12)
+            SVA_PLANE_CASE(13) SVA_PLANE_CASE(14)
+            default: return hipErrorInvalidValue;
+        }
+#undef SVA_PLANE_CASE
+        return hipGetLastError();
+    }
     dim3 grid((unsigned)((npx + 3) / 4));
     switch ((k + 1) / 2) {  // ND = ceil(2k / 4)
         SVA_REF_CASE(1) SVA_REF_CASE(2) SVA_REF_CASE(3) SVA_REF_CASE(4)

@@ -129,3 +129,37 @@ def test_depth(ctx, oracle, torch_dev):
     ctx.disparity_to_depth_d(d.data_ptr(), disp.size, cam_distance, f, ps, out.data_ptr())
     ctx.synchronize()
     assert np.array_equal(out.cpu().numpy(), oracle.disp_to_depth(disp, cam_distance, f, ps))
+
+
+def test_ref_path_plane_fallback_diagonal_jump(ctx, sva, oracle):
+    """Pair 12 -> 0 (two grid units on the diagonal) at 1080p: per-tile offset
+    boxes exceed the plane kernel's bitmap, so those tiles take the per-pixel
+    fallback inside the same launch -- still bit-exact."""
+    W, H, k = 1920, 1080, 20
+    grid = synth.reference_array(0.036 / W)
+    cr, co = sva.Camera.make(*grid[12]), sva.Camera.make(*grid[0])
+    ocr, oco = oracle.OCamera.make(*grid[12]), oracle.OCamera.make(*grid[0])
+    a = synth.texture(H, W, 8)
+    # camera 0 sees the scene shifted by +266..+533 px on both axes here:
+    # only pixels with x, y small enough keep both endpoints in the image
+    b = np.roll(np.roll(a, 400, axis=0), 400, axis=1)
+    mask = np.zeros((H, W), np.uint8)
+    mask[100:104, 300:500] = 1
+    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k, mask=mask)
+    o8, o16, ov, n = oracle.ref_pair(a, b, ocr, oco, k=k, mask=mask)
+    assert n > 0 and ov.sum() > 0
+    assert np.array_equal(valid, ov) and np.array_equal(d16, o16) and np.array_equal(d8, o8)
+
+
+@pytest.mark.parametrize("pair", [(12, 6), (12, 13)])
+def test_ref_path_full_frame_vga(ctx, sva, oracle, pair):
+    """A whole 640x480 frame (the reference's own size class, k = 20) through
+    the offset-plane kernel, bit-exact vs the oracle."""
+    W, H, k = 640, 480, 20
+    cr, co, ocr, oco = cams_for(sva, oracle, W, *pair)
+    a = synth.texture(H, W, pair[1])
+    gx, gy = pair[1] % 5 - 2, pair[1] // 5 - 2
+    b = np.roll(np.roll(a, -60 * gy, axis=0), -60 * gx, axis=1)
+    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k)
+    o8, o16, ov, _ = oracle.ref_pair(a, b, ocr, oco, k=k)
+    assert np.array_equal(valid, ov) and np.array_equal(d16, o16) and np.array_equal(d8, o8)
