@@ -209,8 +209,9 @@ constexpr int PT_ROWS = 32;                  // tile rows
 constexpr int PT_REG_W = 64;                 // region width = TW + 2k
 constexpr int PT_MAXK = 28;                  // TW >= 8
 constexpr int PT_REG_H = PT_ROWS + 2 * PT_MAXK;
-constexpr int PT_CS_W = PT_REG_W + 2;        // padded column-sum rows (bank spread)
-constexpr int PT_MAXBITS = 1 << 16;          // offset bitmap capacity
+constexpr int PT_P_W = PT_REG_W + 1;         // prefix rows: 65 u32 (odd stride spreads banks)
+constexpr int PT_MAXBITS = 1 << 15;          // offset bitmap capacity
+constexpr int PT_OU_BYTES = 28 * 1024;       // staged union of O over all planes (3 workgroups/CU)
 
 __device__ __forceinline__ bool on_line(const Line& L, int cx, int cy) {
     int i, t;
@@ -234,8 +235,9 @@ __global__ __launch_bounds__(256) void ref_plane_kernel(
     uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out) {
     __shared__ __attribute__((aligned(16))) uint8_t Rr[PT_REG_H][PT_REG_W];   // read as dwords
     __shared__ __attribute__((aligned(16))) uint8_t AD[PT_REG_H][PT_REG_W];
-    __shared__ unsigned short CS[PT_ROWS][PT_CS_W];
+    __shared__ unsigned Pf[PT_ROWS][PT_P_W];   // per-row exclusive prefix of column sums
     __shared__ unsigned bits[PT_MAXBITS / 32];
+    __shared__ __attribute__((aligned(16))) uint8_t OU[PT_OU_BYTES];   // O over every plane
     __shared__ int box[4];                    // dx_lo, dx_hi, dy_lo, dy_hi
     const int t = threadIdx.x;
     const int TW = PT_REG_W - 2 * k;
@@ -303,6 +305,19 @@ __global__ __launch_bounds__(256) void ref_plane_kernel(
             atomicOr(&bits[b >> 5], 1u << (b & 31));
         }
     }
+    // Stage O over the union of all planes once, when it fits: rows
+    // ry0 + dylo + [0, RH + bh - 1), cols rx0 + dxlo + [0, 64 + bw - 1); the
+    // plane loop then reads only LDS.  Otherwise each plane loads O itself.
+    const int ouw = (PT_REG_W + bw - 1 + 3) & ~3, ouh = RH + bh - 1;
+    const bool staged = ouw * ouh <= PT_OU_BYTES - 8;   // slack: the realigning read may touch one dword past the region
+    if (staged) {
+        const int ox0 = rx0 + dxlo, oy0 = ry0 + dylo;
+        for (int i = t; i < ouw * ouh; i += 256) {
+            const int v = i / ouw, u = i - v * ouw;
+            const int gx = ox0 + u, gy = oy0 + v;
+            OU[i] = (gx >= 0 && gx < W && gy >= 0 && gy < H) ? other[(size_t)gy * pitch + gx] : 0;
+        }
+    }
     __syncthreads();
     const int cu = t & 63, cseg = t >> 6;    // column-sum thread: column, 8-row segment
     for (int wd = 0; wd < nwords; wd++) {
@@ -317,7 +332,13 @@ __global__ __launch_bounds__(256) void ref_plane_kernel(
                 const int v = i >> 4, u4 = (i & 15) * 4;
                 const int gx = rx0 + u4 + ddx, gy = ry0 + v + ddy;
                 unsigned o;
-                if (gy >= 0 && gy < H && gx >= 0 && gx + 3 < W) {
+                if (staged) {
+                    // bytes OU[(v + ddy - dylo) * ouw + u4 + ddx - dxlo + 0..3], realigned
+                    const int bo = (v + ddy - dylo) * ouw + u4 + (ddx - dxlo);
+                    const unsigned* w = reinterpret_cast<const unsigned*>(OU) + (bo >> 2);
+                    const unsigned sh = (unsigned)(bo & 3);
+                    o = sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
+                } else if (gy >= 0 && gy < H && gx >= 0 && gx + 3 < W) {
                     const uint8_t* src = other + (size_t)gy * pitch + gx;
                     const uintptr_t a = (uintptr_t)src;
                     const unsigned* w = (const unsigned*)(a & ~(uintptr_t)3);
@@ -342,36 +363,44 @@ __global__ __launch_bounds__(256) void ref_plane_kernel(
                 *(unsigned*)&AD[v][u4] = ad;
             }
             __syncthreads();
-            // (b) column sums over 2k rows, 8 output rows per thread
+            // (b) column sums over 2k rows (wave = 8 output rows, lane =
+            // column), each row turned into an exclusive prefix over the 64
+            // columns by a cross-lane scan, so (c) needs two reads per pixel.
+            // (Summing 2k consecutive u16 column sums per pixel instead let
+            // the compiler merge them into unaligned wide LDS loads:
+            // SQ_LDS_UNALIGNED_STALL 3.07G of 3.84G LDS cycles.)
             {
                 const int r0 = cseg * 8;
                 unsigned sacc = 0;
                 for (int v = 0; v < 2 * k; v++) sacc += AD[r0 + v][cu];
-                CS[r0][cu] = (unsigned short)sacc;
 #pragma unroll
-                for (int rr2 = 1; rr2 < 8; rr2++) {
-                    sacc += AD[r0 + rr2 - 1 + 2 * k][cu];
-                    sacc -= AD[r0 + rr2 - 1][cu];
-                    CS[r0 + rr2][cu] = (unsigned short)sacc;
+                for (int rr2 = 0; rr2 < 8; rr2++) {
+                    if (rr2 > 0) {
+                        sacc += AD[r0 + rr2 - 1 + 2 * k][cu];
+                        sacc -= AD[r0 + rr2 - 1][cu];
+                    }
+                    unsigned sc = sacc;              // inclusive scan over the lanes
+#pragma unroll
+                    for (int off = 1; off < 64; off <<= 1) {
+                        const unsigned o = __shfl_up(sc, off, 64);
+                        if (cu >= off) sc += o;
+                    }
+                    Pf[r0 + rr2][cu + 1] = sc;
+                    if (cu == 0) Pf[r0 + rr2][0] = 0;
                 }
             }
             __syncthreads();
-            // (c) row sums, membership, first-minimum key.  Column sums read:
-            // CS[r][xl .. xl + 2k - 1] with xl < TW: index <= TW + 2k - 2 = 62.
-            if (xs < TW) {
-                unsigned sad = 0;
-                for (int u = 0; u < 2 * k; u++) sad += CS[r][xs + u];
+            // (c) SAD from two prefix reads, membership, first-minimum key
 #pragma unroll
-                for (int j = 0; j < MAXPPT; j++) {
-                    if (j >= PPT || xs + j >= TW) break;
-                    if (j > 0) sad += (unsigned)CS[r][xs + j - 1 + 2 * k] - CS[r][xs + j - 1];
-                    if (!ok[j]) continue;
-                    const int cx = tx0 + xs + j + ddx, cy = ty0 + r + ddy;
-                    if (!on_line(Ls[j], cx, cy)) continue;
-                    const unsigned long long key =
-                        ((unsigned long long)sad << 32) | (unsigned)line_index(Ls[j], cx, cy);
-                    best[j] = key < best[j] ? key : best[j];
-                }
+            for (int j = 0; j < MAXPPT; j++) {
+                if (!ok[j]) continue;               // ok[] implies j < PPT, xs + j < TW
+                const int xl = xs + j;
+                const unsigned sad = Pf[r][xl + 2 * k] - Pf[r][xl];
+                const int cx = tx0 + xl + ddx, cy = ty0 + r + ddy;
+                if (!on_line(Ls[j], cx, cy)) continue;
+                const unsigned long long key =
+                    ((unsigned long long)sad << 32) | (unsigned)line_index(Ls[j], cx, cy);
+                best[j] = key < best[j] ? key : best[j];
             }
         }
     }
