@@ -213,6 +213,21 @@ constexpr int PT_P_W = PT_REG_W + 1;         // prefix rows: 65 u32 (odd stride 
 constexpr int PT_MAXBITS = 1 << 15;          // offset bitmap capacity
 constexpr int PT_OU_BYTES = 28 * 1024;       // staged union of O over all planes (3 workgroups/CU)
 
+// Inclusive wave64 scan in 6 DPP adds (no LDS): Hillis-Steele within each
+// 16-lane row (row_shr 1, 2, 4, 8; lanes with no source read 0), then
+// row_bcast:15 adds lane 15 into rows 1 and 3 and row_bcast:31 adds lane 31
+// into rows 2 and 3.  (A ds_bpermute-based __shfl_up scan put 6 LDS
+// round-trips on the dependency chain of every row.)
+__device__ __forceinline__ unsigned scan64_dpp(unsigned v) {
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return v;
+}
+
 __device__ __forceinline__ bool on_line(const Line& L, int cx, int cy) {
     int i, t;
     if (L.high) { i = cy - L.y0; t = L.step * (cx - L.x0); }
@@ -379,12 +394,7 @@ __global__ __launch_bounds__(256) void ref_plane_kernel(
                         sacc += AD[r0 + rr2 - 1 + 2 * k][cu];
                         sacc -= AD[r0 + rr2 - 1][cu];
                     }
-                    unsigned sc = sacc;              // inclusive scan over the lanes
-#pragma unroll
-                    for (int off = 1; off < 64; off <<= 1) {
-                        const unsigned o = __shfl_up(sc, off, 64);
-                        if (cu >= off) sc += o;
-                    }
+                    const unsigned sc = scan64_dpp(sacc);   // inclusive over the lanes
                     Pf[r0 + rr2][cu + 1] = sc;
                     if (cu == 0) Pf[r0 + rr2][0] = 0;
                 }
