@@ -369,13 +369,12 @@ __global__ __launch_bounds__(256) void ref_plane_kernel(
                     }
                 }
                 const unsigned rr = *(const unsigned*)&Rr[v][u4];
-                unsigned ad = 0;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int d = (int)((o >> (8 * q)) & 0xff) - (int)((rr >> (8 * q)) & 0xff);
-                    ad |= (unsigned)(d < 0 ? -d : d) << (8 * q);
-                }
-                *(unsigned*)&AD[v][u4] = ad;
+                // |o - r| per byte on even / odd bytes as u16 pairs: max - min
+                const u16x2 oe = as_v2(o & 0x00ff00ffu), oo = as_v2((o >> 8) & 0x00ff00ffu);
+                const u16x2 re = as_v2(rr & 0x00ff00ffu), ro = as_v2((rr >> 8) & 0x00ff00ffu);
+                const unsigned de = as_u32(__builtin_elementwise_max(oe, re) - vmin2(oe, re));
+                const unsigned dd = as_u32(__builtin_elementwise_max(oo, ro) - vmin2(oo, ro));
+                *(unsigned*)&AD[v][u4] = de | (dd << 8);
             }
             __syncthreads();
             // (b) column sums over 2k rows (wave = 8 output rows, lane =
