@@ -153,30 +153,47 @@ __global__ void d2p_count_kernel(const double* __restrict__ depth, int W, int H,
     counts[(size_t)u * nch + ch] = n;   // column-major unit order
 }
 
+// Inclusive wave64 scan in 6 DPP adds (row_shr 1/2/4/8, row_bcast 15/31).
+__device__ __forceinline__ unsigned wave_scan_incl(unsigned v) {
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+
 // One block: exclusive scan of counts[0..n) in place; total -> *total.
+// Rounds of 1024 consecutive counts (one coalesced load per thread), a DPP
+// wave scan, the 16 wave totals combined through LDS, and a running carry.
+// (A per-thread walk over 32 contiguous counts serialised the loads: 58 us.)
 __global__ __launch_bounds__(1024) void d2p_scan_kernel(unsigned* __restrict__ counts, int n,
                                                        long long* __restrict__ total) {
-    __shared__ unsigned long long part[1024];
-    const int t = threadIdx.x;
-    const int per = (n + 1023) / 1024;
-    const int b = t * per, e = min(n, b + per);
-    unsigned long long s = 0;
-    for (int i = b; i < e; i++) s += counts[i];
-    part[t] = s;
+    __shared__ unsigned wsum[16];
+    __shared__ unsigned long long carry_s;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if (t == 0) carry_s = 0;
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {   // Hillis-Steele inclusive scan
-        unsigned long long v = t >= off ? part[t - off] : 0;
+    for (int base = 0; base < n; base += 1024) {
+        const int i = base + t;
+        const unsigned c = i < n ? counts[i] : 0u;
+        const unsigned incl = wave_scan_incl(c);
+        if (lane == 63) wsum[wave] = incl;
         __syncthreads();
-        part[t] += v;
+        unsigned before = 0, round = 0;
+        for (int w = 0; w < 16; w++) {
+            const unsigned ws = wsum[w];
+            if (w < wave) before += ws;
+            round += ws;
+        }
+        const unsigned long long carry = carry_s;
+        if (i < n) counts[i] = (unsigned)(carry + before + incl - c);
+        __syncthreads();                      // everyone has read wsum / carry_s
+        if (t == 0) carry_s = carry + round;
         __syncthreads();
     }
-    unsigned long long run = t ? part[t - 1] : 0;
-    for (int i = b; i < e; i++) {
-        const unsigned c = counts[i];
-        counts[i] = (unsigned)run;
-        run += c;
-    }
-    if (t == 1023) *total = (long long)part[1023];
+    if (t == 0) *total = (long long)carry_s;
 }
 
 __global__ void d2p_write_kernel(const double* __restrict__ depth, int W, int H, int nch,

@@ -34,6 +34,8 @@ for step in "$@"; do
     pmc4k) run pmc4k_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc4k_fetch -o run --output-format csv -- python3 bench.py --workload 4k_d256 --steps 2 --warmup 1 --no-cpu-baseline
            run pmc4k_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc4k_write -o run --output-format csv -- python3 bench.py --workload 4k_d256 --steps 2 --warmup 1 --no-cpu-baseline
            run pmc4k_json 120 python3 tools/pmc_traffic.py gpurun_out/pmc4k_fetch gpurun_out/pmc4k_write 3840 2160 256 gpurun_out/pmc_4k_d256.json ;;
+    prof_refpath) run prof_refpath 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_refpath -o run --output-format csv -- python3 tools/bench_refpath.py --reps 3 --cpu-rows 2 ;;
+    prof_refine) run prof_refine 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_refine -o run --output-format csv -- python3 tools/bench_refine.py ;;
     pmcjson) run pmcjson 120 python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write 1920 1080 128 gpurun_out/pmc_1080p_d128.json ;;
     prof_center8) run prof_center8 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_center8 -o run --output-format csv -- python3 bench.py --workload center8 --steps 5 --warmup 2 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
