@@ -247,9 +247,9 @@ int run_improve(Ctx* c, const uint8_t* disp, const uint8_t* center, const uint8_
         int s;
         if (fetch && (s = fetch(i, &img))) return s;
         // the reference's shifted Mat is uninitialised; DESIGN.md §2.7 fixes it to 0
-        SVA_HIP(c, hipMemsetAsync(sh, 0, bytes, c->stream), "memset");
+        // (zero_fill: the shift kernel writes the 0 of every untouched pixel)
         SVA_HIP(c, launch_shift_perspective(*c, cams[2 * i], cams[2 * i + 1], disp, img, W, H,
-                                            pitch, sh), "shift launch");
+                                            pitch, sh, true), "shift launch");
         SVA_HIP(c, launch_refine(*c, disp, center, sh, mask, W, H, pitch, k, cams[2 * i],
                                  cams[2 * i + 1], out, fault), "refine launch");
     }

@@ -116,7 +116,7 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
 // refine.hip
 hipError_t launch_shift_perspective(Ctx& c, const sva_camera& in, const sva_camera& out,
                                     const uint8_t* disp, const uint8_t* img, int W, int H,
-                                    size_t pitch, uint8_t* shifted);
+                                    size_t pitch, uint8_t* shifted, bool zero_fill = false);
 hipError_t launch_refine(Ctx& c, const uint8_t* disp, const uint8_t* center,
                          const uint8_t* shifted, const uint8_t* mask, int W, int H, size_t pitch,
                          int k, const sva_camera& c0, const sva_camera& c1, uint8_t* out,

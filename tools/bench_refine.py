@@ -81,6 +81,14 @@ def main():
                       "cpu_sample": f"24 mask rows x 600 px x 4 pairs, {cdt:.2f} s",
                       "speedup": round((npx / dt) / (cpx / cdt), 1)}), flush=True)
 
+    # the same without a mask: every pixel whose windows fit (the rest are skipped)
+    dt, ks = timed(lambda: ctx.improve_with_disparity_d(
+        d_disp.data_ptr(), d_center.data_ptr(), [o.data_ptr() for o in d_others], pairs, W, H, W,
+        None, 21, False, out.data_ptr()), ["shift_perspective", "refine"])
+    print(json.dumps({"routine": "improveWithDisparity_nomask", "size": f"{W}x{H}", "pairs": 4,
+                      "gpu_ms": round(dt * 1e3, 3), "kernels_ms": ks,
+                      "gpu_Mpx_pair_per_s": round(W * H * 4 / dt / 1e6, 1)}), flush=True)
+
     # shiftPerspective2 / Points3DToDepthMap / DepthMapToPoints3D
     depth = rng.uniform(0.3, 3.0, size=(H, W))
     d_depth = torch.from_numpy(depth).to(dev)
