@@ -67,6 +67,48 @@ def test_improve_with_disparity_windows(ctx, sva, oracle, window):
     assert np.array_equal(got, exp)
 
 
+@pytest.mark.parametrize("W,H,window", [(37, 23, 3), (301, 77, 21), (301, 77, 33),
+                                          (301, 77, 35), (130, 70, 2)])
+def test_improve_padded_pitch_sparse_mask(ctx, sva, oracle, torch_dev, W, H, window):
+    """Device entry point on planes with pitch > W and random bytes in the
+    padding.  Cases:
+    * the box kernel's strip / band edges, including images smaller than one strip;
+    * k = 16, the last box size, against k = 17 on the direct kernel;
+    * horizontal, vertical and diagonal steps;
+    * a 2% mask, so most strips are skipped.
+    The output padding stays untouched."""
+    P = W + 13
+    rng = np.random.default_rng(W * 1000 + window)
+    center = synth.texture(H, W, 3)
+    pairs, opairs, imgs = [], [], []
+    for i, b in enumerate((13, 7, 18, 6)):
+        ci, co, oi, oo = rig_pair(sva, oracle, 12, b, W)
+        pairs.append((ci, co)); opairs.append((oi, oo))
+        imgs.append(synth.texture(H, W, 60 + i))
+    disp = rng.integers(0, 12, size=(H, W)).astype(np.uint8)
+    mask = (rng.random((H, W)) < 0.02).astype(np.uint8)
+    init = rng.integers(0, 256, size=(H, W)).astype(np.uint8)
+
+    def padded(a):
+        full = rng.integers(0, 256, size=(H, P)).astype(np.uint8)
+        full[:, :W] = a
+        return torch.from_numpy(full).to(torch_dev)
+
+    dd, dc, dm = padded(disp), padded(center), padded(mask)
+    di = [padded(im) for im in imgs]
+    out = padded(init)
+    pad_before = out[:, W:].cpu().numpy().copy()
+    ctx.improve_with_disparity_d(dd.data_ptr(), dc.data_ptr(), [t.data_ptr() for t in di], pairs,
+                                 W, H, P, dm.data_ptr(), window, False, out.data_ptr())
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    st, exp = oracle.improve_with_disparity(disp, center, imgs, opairs, window=window, mask=mask,
+                                            init=init)
+    got = out.cpu().numpy()
+    assert np.array_equal(got[:, :W], exp)
+    assert np.array_equal(got[:, W:], pad_before)
+
+
 def test_improve_finds_known_correction(ctx, sva, oracle):
     W, H, d0 = 200, 80, 9
     center, img = _refine_case(H, W, d0, 3, 5)
