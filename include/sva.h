@@ -218,6 +218,32 @@ int sva_resize_half_d(void* ctx, const uint8_t* src, int width, int height, size
 int sva_resize_half(void* ctx, const uint8_t* src, int width, int height, size_t pitch,
                     uint8_t* dst, size_t dst_pitch);
 
+/* ------------------------------------------ evaluation --
+ * The reference's ground-truth comparison (CameraStereoVision.cpp:107-110,
+ * 118-119) and calculateAverageError (functions.cpp:348-354), on dense
+ * row-major f64 matrices.  OpenCV 4.2 semantics restated (DESIGN.md §2.8;
+ * OpenCV absent: parity unpinned):
+ *   sva_resize_linear_f64: resize(src, dst, Size(dw, dh)), INTER_LINEAR --
+ *     copy at equal size, the area path at exactly 2x, else float-coefficient
+ *     bilinear taps (x clamped, y rows clipped).
+ *   sva_ref_error: error = (resize(depth, ref.size()) - ref) * scale,
+ *     evaluated as OpenCV's addWeighted: a * scale + b * (-scale) + 0.
+ *   sva_masked_mean: cv::mean(image, mask)[0]; mask nullable (= all pixels);
+ *     0 for an empty mask.  *mean is a HOST pointer in both forms (the _d form
+ *     synchronises the context stream). */
+int sva_resize_linear_f64_d(void* ctx, const double* src, int src_w, int src_h, double* dst,
+                            int dst_w, int dst_h);
+int sva_resize_linear_f64(void* ctx, const double* src, int src_w, int src_h, double* dst,
+                          int dst_w, int dst_h);
+int sva_ref_error_d(void* ctx, const double* depth, int width, int height, const double* ref,
+                    int ref_w, int ref_h, double scale, double* error);
+int sva_ref_error(void* ctx, const double* depth, int width, int height, const double* ref,
+                  int ref_w, int ref_h, double scale, double* error);
+int sva_masked_mean_d(void* ctx, const double* image, const uint8_t* mask, int width, int height,
+                      double* mean);
+int sva_masked_mean(void* ctx, const double* image, const uint8_t* mask, int width, int height,
+                    double* mean);
+
 /* Multi-pair depth fusion on the root: per
  * pixel the median of baseline_i * f / (disp_i * pixel_size) over the maps
  * with disp_i != invalid and disp_i > 0 (mean of the middle two for an even

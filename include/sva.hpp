@@ -12,6 +12,9 @@
 //   computeDisparity     NEW: replaces the inline hot loop
 //                        src/CameraStereoVision.cpp:44-95 with one GPU call
 //   disparityToDepth     src/CameraStereoVision.cpp:47,98-100
+//   getIdealRef / saveImage / loadImage / calculateAverageError
+//                        src/functions.cpp:323-354 (OpenCV-YAML matrix files),
+//   refError             src/CameraStereoVision.cpp:107-110,118-119
 // Host-side helpers (Camera math, bresenham, pair tables) run on the CPU as in
 // the reference -- they are per-call scalars, not the hot path.  Everything
 // per-pixel runs on the GPU through sva.h.  Errors are reported as
@@ -24,7 +27,10 @@
 #include <filesystem>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
+#include <fstream>
+#include <sstream>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -516,6 +522,167 @@ inline std::vector<uint8_t> resizeHalf(Engine& eng, const ImageView& img, int* o
     if (outW) *outW = dw;
     if (outH) *outH = dh;
     return out;
+}
+
+// ---- evaluation ---------------------------------------
+
+// A matrix of an OpenCV FileStorage "!!opencv-matrix" node: rows x cols x
+// channels values of element code dt ('u' 'c' 'w' 's' 'i' 'f' 'd'), held as
+// doubles (exact for every one of those types).
+struct YamlMatrix {
+    int rows = 0, cols = 0, channels = 1;
+    char dt = 'd';
+    std::vector<double> data;   // row-major, channels interleaved
+};
+
+namespace detail {
+inline double yaml_number(const std::string& t) {
+    if (t == ".Inf" || t == ".inf" || t == "+.Inf") return HUGE_VAL;
+    if (t == "-.Inf" || t == "-.inf") return -HUGE_VAL;
+    if (t == ".Nan" || t == ".nan" || t == ".NaN") return std::nan("");
+    size_t used = 0;
+    const double v = std::stod(t, &used);
+    if (used != t.size()) throw Error(SVA_ERR_INVALID_ARG, "yaml: bad number '" + t + "'");
+    return v;
+}
+inline std::string yaml_field(const std::string& body, const std::string& name) {
+    std::istringstream in(body);
+    std::string line;
+    while (std::getline(in, line)) {
+        const size_t a = line.find_first_not_of(" \t");
+        if (a == std::string::npos || a == 0) continue;   // nested fields are indented
+        if (line.compare(a, name.size() + 1, name + ":") == 0) {
+            std::string v = line.substr(a + name.size() + 1);
+            v.erase(0, v.find_first_not_of(" \t\""));
+            v.erase(v.find_last_not_of(" \t\"\r") + 1);
+            return v;
+        }
+    }
+    throw Error(SVA_ERR_INVALID_ARG, "yaml: missing field " + name);
+}
+}  // namespace detail
+
+// FileStorage(path, READ)[key] >> Mat for an "!!opencv-matrix" node.
+inline YamlMatrix readYamlMatrix(const std::string& path, const std::string& key) {
+    std::ifstream f(path);
+    if (!f) throw Error(SVA_ERR_INVALID_ARG, "cannot open " + path);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    const std::string text = ss.str();
+    const std::string head = key + ":";
+    size_t pos = 0, start = std::string::npos;
+    while ((pos = text.find(head, pos)) != std::string::npos) {
+        const bool bol = pos == 0 || text[pos - 1] == '\n';
+        const size_t eol = text.find('\n', pos);
+        const std::string rest = text.substr(pos + head.size(), eol - pos - head.size());
+        if (bol && rest.find("!!opencv-matrix") != std::string::npos) {
+            start = eol;
+            break;
+        }
+        pos += head.size();
+    }
+    if (start == std::string::npos) throw Error(SVA_ERR_INVALID_ARG, "yaml: no matrix " + key);
+    // the node ends at the next unindented line
+    size_t end = start;
+    while (end < text.size()) {
+        const size_t nl = text.find('\n', end + 1);
+        const size_t ls = end + 1;
+        if (ls < text.size() && text[ls] != ' ' && text[ls] != '\t' && text[ls] != '\n') break;
+        if (nl == std::string::npos) { end = text.size(); break; }
+        end = nl;
+    }
+    const std::string body = text.substr(start, end - start);
+    YamlMatrix m;
+    m.rows = std::stoi(detail::yaml_field(body, "rows"));
+    m.cols = std::stoi(detail::yaml_field(body, "cols"));
+    const std::string dt = detail::yaml_field(body, "dt");
+    if (dt.empty() || std::string("ucwsifd").find(dt.back()) == std::string::npos)
+        throw Error(SVA_ERR_INVALID_ARG, "yaml: unsupported dt " + dt);
+    m.dt = dt.back();
+    m.channels = dt.size() > 1 ? std::stoi(dt.substr(0, dt.size() - 1)) : 1;
+    const size_t lb = body.find('['), rb = body.find(']', lb);
+    if (lb == std::string::npos || rb == std::string::npos)
+        throw Error(SVA_ERR_INVALID_ARG, "yaml: missing data");
+    std::string tok;
+    for (size_t i = lb + 1; i <= rb; i++) {
+        const char ch = body[i];
+        if (ch == ',' || ch == ']' || ch == ' ' || ch == '\n' || ch == '\t' || ch == '\r') {
+            if (!tok.empty()) m.data.push_back(detail::yaml_number(tok));
+            tok.clear();
+        } else {
+            tok += ch;
+        }
+    }
+    if (m.data.size() != (size_t)m.rows * m.cols * m.channels)
+        throw Error(SVA_ERR_INVALID_ARG, "yaml: data size does not match rows x cols");
+    return m;
+}
+
+// FileStorage(path, WRITE) << key << Mat (a new file holding one node).
+inline void writeYamlMatrix(const std::string& path, const std::string& key, const YamlMatrix& m) {
+    if (m.data.size() != (size_t)m.rows * m.cols * m.channels)
+        throw Error(SVA_ERR_INVALID_ARG, "yaml: data size does not match rows x cols");
+    std::ofstream f(path);
+    if (!f) throw Error(SVA_ERR_INVALID_ARG, "cannot write " + path);
+    f << "%YAML:1.0\n---\n" << key << ": !!opencv-matrix\n   rows: " << m.rows
+      << "\n   cols: " << m.cols << "\n   dt: ";
+    if (m.channels > 1) f << m.channels;
+    f << m.dt << "\n   data: [ ";
+    const bool fl = m.dt == 'f' || m.dt == 'd';
+    char buf[64];
+    for (size_t i = 0; i < m.data.size(); i++) {
+        const double v = m.data[i];
+        if (fl && std::isnan(v)) std::snprintf(buf, sizeof buf, ".Nan");
+        else if (fl && std::isinf(v)) std::snprintf(buf, sizeof buf, v > 0 ? ".Inf" : "-.Inf");
+        else if (fl) std::snprintf(buf, sizeof buf, m.dt == 'f' ? "%.9g" : "%.17g", v);
+        else std::snprintf(buf, sizeof buf, "%lld", (long long)v);
+        f << buf << (i + 1 < m.data.size() ? ((i + 1) % 8 ? ", " : ",\n       ") : "");
+    }
+    f << " ]\n";
+}
+
+// getIdealRef -- functions.cpp:323-329 ("idealRef.yml", key "R").
+inline YamlMatrix getIdealRef(const std::string& path = "idealRef.yml") {
+    return readYamlMatrix(path, "R");
+}
+// saveImage / loadImage -- functions.cpp:331-346 (key "image").
+inline void saveImage(const std::string& filename, const YamlMatrix& image) {
+    writeYamlMatrix(filename, "image", image);
+}
+inline YamlMatrix loadImage(const std::string& filename) { return readYamlMatrix(filename, "image"); }
+
+// resize(src, dst, Size(dw, dh)) INTER_LINEAR on a dense f64 matrix, on the GPU.
+inline std::vector<double> resizeLinear(Engine& eng, const std::vector<double>& src, int sw, int sh,
+                                        int dw, int dh) {
+    if (src.size() != (size_t)sw * sh) throw Error(SVA_ERR_INVALID_ARG, "resize: size mismatch");
+    std::vector<double> out((size_t)dw * dh);
+    eng.check(sva_resize_linear_f64(eng.handle(), src.data(), sw, sh, out.data(), dw, dh));
+    return out;
+}
+
+// CameraStereoVision.cpp:107-110,118-119: resize(depth, depth2, ref.size());
+// error = (depth2 - ref) * scale -- on the GPU, returned at ref's size.
+inline std::vector<double> refError(Engine& eng, const std::vector<double>& depth, int w, int h,
+                                    const YamlMatrix& ref, double scale = 50.0) {
+    if (depth.size() != (size_t)w * h || ref.channels != 1 ||
+        ref.data.size() != (size_t)ref.rows * ref.cols)
+        throw Error(SVA_ERR_INVALID_ARG, "refError: size mismatch");
+    std::vector<double> err(ref.data.size());
+    eng.check(sva_ref_error(eng.handle(), depth.data(), w, h, ref.data.data(), ref.cols, ref.rows,
+                            scale, err.data()));
+    return err;
+}
+
+// calculateAverageError -- functions.cpp:348-354: cv::mean(image, mask)[0] on
+// the GPU.  mask (W*H, nullable = all) replaces dlib's getFaceMask.
+inline double calculateAverageError(Engine& eng, const std::vector<double>& image, int w, int h,
+                                    const std::vector<uint8_t>* mask = nullptr) {
+    if (image.size() != (size_t)w * h || (mask && mask->size() != image.size()))
+        throw Error(SVA_ERR_INVALID_ARG, "calculateAverageError: size mismatch");
+    double mean = 0;
+    eng.check(sva_masked_mean(eng.handle(), image.data(), mask ? mask->data() : nullptr, w, h,
+                              &mean));
+    return mean;
 }
 
 }  // namespace sva

@@ -69,6 +69,9 @@ def _load():
         "svo_depth_to_points": (ct.c_int64, [vp, i32, i32, P(OCamera), vp]),
         "svo_resize_half_size": (None, [i32, i32, P(i32), P(i32)]),
         "svo_resize_half": (None, [vp, i32, i32, ct.c_ssize_t, vp, ct.c_ssize_t]),
+        "svo_resize_linear_f64": (None, [vp, i32, i32, vp, i32, i32]),
+        "svo_ref_error": (None, [vp, i32, i32, vp, i32, i32, ct.c_double, vp]),
+        "svo_masked_mean": (ct.c_double, [vp, vp, i32, i32]),
     }
     for n, (r, a) in sig.items():
         f = getattr(lib, n)
@@ -306,3 +309,28 @@ def resize_half(img):
     out = np.zeros((dh.value, dw.value), np.uint8)
     lib.svo_resize_half(_p(img), W, H, W, _p(out), max(1, dw.value))
     return out
+
+
+def resize_linear_f64(src, dw, dh):
+    src = _c(src, np.float64)
+    sh, sw = src.shape
+    out = np.zeros((dh, dw), np.float64)
+    lib.svo_resize_linear_f64(_p(src), sw, sh, _p(out), dw, dh)
+    return out
+
+
+def ref_error(depth, ref, scale=50.0):
+    depth = _c(depth, np.float64)
+    ref = _c(ref, np.float64)
+    h, w = depth.shape
+    rh, rw = ref.shape
+    out = np.zeros((rh, rw), np.float64)
+    lib.svo_ref_error(_p(depth), w, h, _p(ref), rw, rh, scale, _p(out))
+    return out
+
+
+def masked_mean(image, mask=None):
+    image = _c(image, np.float64)
+    h, w = image.shape
+    m = None if mask is None else _c(mask, np.uint8)
+    return lib.svo_masked_mean(_p(image), _p(m), w, h)

@@ -175,6 +175,15 @@ void svo_resize_half_size(int W, int H, int* dw, int* dh);
 void svo_resize_half(const uint8_t* src, int W, int H, ptrdiff_t pitch, uint8_t* dst,
                      ptrdiff_t dpitch);
 
+/* Evaluation (eval_oracle.c, OpenCV restated, parity
+ * unpinned): resize(src, dst, Size(dw, dh)) INTER_LINEAR on dense f64,
+ * error = resize(depth, ref.size()) * scale + ref * -scale + 0, and
+ * cv::mean(image, mask)[0] (mask nullable = all). */
+void svo_resize_linear_f64(const double* src, int sw, int sh, double* dst, int dw, int dh);
+void svo_ref_error(const double* depth, int w, int h, const double* ref, int rw, int rh,
+                   double scale, double* error);
+double svo_masked_mean(const double* image, const uint8_t* mask, int w, int h);
+
 #ifdef __cplusplus
 }
 #endif

@@ -41,7 +41,8 @@ EXPORTED = [
     "sva_improve_with_disparity", "sva_shift_perspective2_d", "sva_shift_perspective2",
     "sva_points_to_depth_d", "sva_points_to_depth", "sva_depth_to_points_d",
     "sva_depth_to_points", "sva_resize_half_size", "sva_resize_half_d", "sva_resize_half",
-    "sva_batch_sgm",
+    "sva_batch_sgm", "sva_resize_linear_f64_d", "sva_resize_linear_f64", "sva_ref_error_d",
+    "sva_ref_error", "sva_masked_mean_d", "sva_masked_mean",
 ]
 
 
@@ -152,6 +153,12 @@ def _load() -> ct.CDLL:
         "sva_resize_half_d": (i32, [vp, vp, i32, i32, sz, vp, sz]),
         "sva_resize_half": (i32, [vp, vp, i32, i32, sz, vp, sz]),
         "sva_batch_sgm": (i32, [P(vp), i32, P(PairJob), i32, P(SgmParams)]),
+        "sva_resize_linear_f64_d": (i32, [vp, vp, i32, i32, vp, i32, i32]),
+        "sva_resize_linear_f64": (i32, [vp, vp, i32, i32, vp, i32, i32]),
+        "sva_ref_error_d": (i32, [vp, vp, i32, i32, vp, i32, i32, ct.c_double, vp]),
+        "sva_ref_error": (i32, [vp, vp, i32, i32, vp, i32, i32, ct.c_double, vp]),
+        "sva_masked_mean_d": (i32, [vp, vp, vp, i32, i32, P(ct.c_double)]),
+        "sva_masked_mean": (i32, [vp, vp, vp, i32, i32, P(ct.c_double)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -388,6 +395,48 @@ class Context:
 
     def resize_half_d(self, src, W, H, pitch, dst, dst_pitch):
         self._chk(lib.sva_resize_half_d(self.h, _ptr(src), W, H, pitch, _ptr(dst), dst_pitch))
+
+    # ---- evaluation (CameraStereoVision.cpp:107-119) ----
+    def resize_linear(self, src, dw: int, dh: int):
+        """resize(src, dst, Size(dw, dh)) INTER_LINEAR on a f64 matrix."""
+        src = np.ascontiguousarray(src, dtype=np.float64)
+        sh, sw = src.shape
+        out = np.zeros((dh, dw), np.float64)
+        self._chk(lib.sva_resize_linear_f64(self.h, _ptr(src), sw, sh, _ptr(out), dw, dh))
+        return out
+
+    def resize_linear_d(self, src, sw, sh, dst, dw, dh):
+        self._chk(lib.sva_resize_linear_f64_d(self.h, _ptr(src), sw, sh, _ptr(dst), dw, dh))
+
+    def ref_error(self, depth, ref, scale: float = 50.0):
+        """(resize(depth, ref.size()) - ref) * scale, as the reference's
+        ``Mat error = (depth2 - ref) * 50``."""
+        depth = np.ascontiguousarray(depth, dtype=np.float64)
+        ref = np.ascontiguousarray(ref, dtype=np.float64)
+        h, w = depth.shape
+        rh, rw = ref.shape
+        out = np.zeros((rh, rw), np.float64)
+        self._chk(lib.sva_ref_error(self.h, _ptr(depth), w, h, _ptr(ref), rw, rh, scale,
+                                    _ptr(out)))
+        return out
+
+    def ref_error_d(self, depth, w, h, ref, rw, rh, scale, error):
+        self._chk(lib.sva_ref_error_d(self.h, _ptr(depth), w, h, _ptr(ref), rw, rh, scale,
+                                      _ptr(error)))
+
+    def masked_mean(self, image, mask=None) -> float:
+        """cv::mean(image, mask)[0] (calculateAverageError, functions.cpp:348-354)."""
+        image = np.ascontiguousarray(image, dtype=np.float64)
+        h, w = image.shape
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        out = ct.c_double(0)
+        self._chk(lib.sva_masked_mean(self.h, _ptr(image), _ptr(m), w, h, ct.byref(out)))
+        return out.value
+
+    def masked_mean_d(self, image, mask, w, h) -> float:
+        out = ct.c_double(0)
+        self._chk(lib.sva_masked_mean_d(self.h, _ptr(image), _ptr(mask), w, h, ct.byref(out)))
+        return out.value
 
     def fuse_depth(self, disps: np.ndarray, baselines, f, pixel_size, invalid=0xFFFF):
         d = np.ascontiguousarray(disps, dtype=np.uint16)

@@ -917,6 +917,108 @@ int sva_resize_half(void* ctx, const uint8_t* src, int W, int H, size_t pitch, u
     return SVA_OK;
 }
 
+// ----------------------------------------------------------- evaluation --
+namespace {
+int check_dims(Ctx* c, int w, int h) {
+    if (w <= 0 || h <= 0 || (size_t)w * h > ((size_t)1 << 31))
+        return fail(c, SVA_ERR_INVALID_ARG, "matrix dimensions must be positive (< 2^31 elements)");
+    return SVA_OK;
+}
+
+// Host-buffer form of the resize / error entry points: upload, run, download.
+int host_resize(Ctx* c, const double* src, int sw, int sh, const double* ref, int dw, int dh,
+                double scale, double* dst) {
+    const size_t sb = (size_t)sw * sh * 8, db = (size_t)dw * dh * 8;
+    SVA_HIP(c, c->in_a.ensure(sb), "staging");
+    SVA_HIP(c, c->out_a.ensure(db), "staging");
+    if (ref) SVA_HIP(c, c->in_b.ensure(db), "staging");
+    hipStream_t st = c->stream;
+    SVA_HIP(c, hipMemcpyAsync(c->in_a.ptr, src, sb, hipMemcpyHostToDevice, st), "upload");
+    if (ref) SVA_HIP(c, hipMemcpyAsync(c->in_b.ptr, ref, db, hipMemcpyHostToDevice, st), "upload");
+    SVA_HIP(c, launch_resize_linear(*c, (double*)c->in_a.ptr, sw, sh, (double*)c->out_a.ptr, dw, dh,
+                                    ref ? (double*)c->in_b.ptr : nullptr, scale), "resize launch");
+    SVA_HIP(c, hipMemcpyAsync(dst, c->out_a.ptr, db, hipMemcpyDeviceToHost, st), "download");
+    SVA_HIP(c, hipStreamSynchronize(st), "sync");
+    return SVA_OK;
+}
+}  // namespace
+
+int sva_resize_linear_f64_d(void* ctx, const double* src, int sw, int sh, double* dst, int dw,
+                            int dh) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_dims(c, sw, sh)) || (s = check_dims(c, dw, dh))) return s;
+    if (!src || !dst) return fail(c, SVA_ERR_INVALID_ARG, "null matrix");
+    SVA_HIP(c, launch_resize_linear(*c, src, sw, sh, dst, dw, dh, nullptr, 0.0), "resize launch");
+    return SVA_OK;
+}
+
+int sva_resize_linear_f64(void* ctx, const double* src, int sw, int sh, double* dst, int dw,
+                          int dh) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_dims(c, sw, sh)) || (s = check_dims(c, dw, dh))) return s;
+    if (!src || !dst) return fail(c, SVA_ERR_INVALID_ARG, "null matrix");
+    return host_resize(c, src, sw, sh, nullptr, dw, dh, 0.0, dst);
+}
+
+int sva_ref_error_d(void* ctx, const double* depth, int w, int h, const double* ref, int rw,
+                    int rh, double scale, double* error) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_dims(c, w, h)) || (s = check_dims(c, rw, rh))) return s;
+    if (!depth || !ref || !error) return fail(c, SVA_ERR_INVALID_ARG, "null matrix");
+    SVA_HIP(c, launch_resize_linear(*c, depth, w, h, error, rw, rh, ref, scale), "resize launch");
+    return SVA_OK;
+}
+
+int sva_ref_error(void* ctx, const double* depth, int w, int h, const double* ref, int rw, int rh,
+                  double scale, double* error) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_dims(c, w, h)) || (s = check_dims(c, rw, rh))) return s;
+    if (!depth || !ref || !error) return fail(c, SVA_ERR_INVALID_ARG, "null matrix");
+    return host_resize(c, depth, w, h, ref, rw, rh, scale, error);
+}
+
+int sva_masked_mean_d(void* ctx, const double* image, const uint8_t* mask, int w, int h,
+                      double* mean) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_dims(c, w, h))) return s;
+    if (!image || !mean) return fail(c, SVA_ERR_INVALID_ARG, "null argument");
+    SVA_HIP(c, c->scratch_u16.ensure(masked_mean_workspace()), "reduction workspace");
+    double* dmean = (double*)((char*)c->scratch_u16.ptr + masked_mean_workspace() - sizeof(double));
+    SVA_HIP(c, launch_masked_mean(*c, image, mask, (size_t)w * h, c->scratch_u16.ptr, dmean),
+            "mean launch");
+    SVA_HIP(c, hipMemcpyAsync(mean, dmean, sizeof(double), hipMemcpyDeviceToHost, c->stream),
+            "download");
+    SVA_HIP(c, hipStreamSynchronize(c->stream), "sync");
+    return SVA_OK;
+}
+
+int sva_masked_mean(void* ctx, const double* image, const uint8_t* mask, int w, int h,
+                    double* mean) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_dims(c, w, h))) return s;
+    if (!image || !mean) return fail(c, SVA_ERR_INVALID_ARG, "null argument");
+    const size_t n = (size_t)w * h;
+    SVA_HIP(c, c->in_a.ensure(n * 8), "staging");
+    SVA_HIP(c, c->in_mask.ensure(mask ? n : 1), "staging");
+    hipStream_t st = c->stream;
+    SVA_HIP(c, hipMemcpyAsync(c->in_a.ptr, image, n * 8, hipMemcpyHostToDevice, st), "upload");
+    if (mask) SVA_HIP(c, hipMemcpyAsync(c->in_mask.ptr, mask, n, hipMemcpyHostToDevice, st), "upload");
+    return sva_masked_mean_d(ctx, (double*)c->in_a.ptr, mask ? (uint8_t*)c->in_mask.ptr : nullptr, w,
+                             h, mean);
+}
+
 // ---------------------------------------------------------------- batch --
 int sva_batch_sgm(void** ctxs, int n_ctx, const sva_pair_job* jobs, int n_jobs,
                   const sva_sgm_params* p) {

@@ -132,6 +132,13 @@ hipError_t launch_depth_to_points(Ctx& c, const double* depth, int W, int H,
                                   double* pts);
 // ingest.hip
 void resize_half_size(int W, int H, int* dw, int* dh);
+// evaluation (evaluate.hip): resize(src, dst, Size(dw, dh)) INTER_LINEAR on
+// dense f64; with ref non-null dst = resized * scale + ref * -scale + 0.
+hipError_t launch_resize_linear(Ctx& c, const double* src, int sw, int sh, double* dst, int dw,
+                                int dh, const double* ref, double scale);
+size_t masked_mean_workspace();
+hipError_t launch_masked_mean(Ctx& c, const double* img, const uint8_t* mask, size_t n,
+                              void* ws, double* mean);
 hipError_t launch_resize_half(Ctx& c, const uint8_t* src, int W, int H, size_t pitch,
                               uint8_t* dst, size_t dpitch);
 hipError_t launch_disp_to_depth(Ctx& c, const uint8_t* disp, int n, double cam_distance,

@@ -28,7 +28,45 @@ static std::vector<Camera> rig(int W) {
     return cams;
 }
 
+static void yaml_tests() {
+    // getIdealRef / saveImage / loadImage (functions.cpp:323-346): OpenCV's own text
+    const std::string dir = std::filesystem::temp_directory_path().string();
+    const std::string p = dir + "/sva_test_idealRef.yml";
+    {
+        std::ofstream f(p);
+        f << "%YAML:1.0\n---\nR: !!opencv-matrix\n   rows: 2\n   cols: 3\n   dt: d\n"
+             "   data: [ 1., 2.5000000000000000e+00, -3.2500000000000000e+00, .Inf,\n"
+             "       -.Inf, .Nan ]\nimage: !!opencv-matrix\n   rows: 1\n   cols: 2\n"
+             "   dt: \"3u\"\n   data: [ 1, 2, 3, 4, 5, 255 ]\n";
+    }
+    YamlMatrix R = getIdealRef(p);
+    CHECK(R.rows == 2 && R.cols == 3 && R.dt == 'd' && R.data.size() == 6);
+    CHECK(R.data[0] == 1.0 && R.data[1] == 2.5 && R.data[2] == -3.25);
+    CHECK(std::isinf(R.data[3]) && R.data[3] > 0 && std::isinf(R.data[4]) && R.data[4] < 0);
+    CHECK(std::isnan(R.data[5]));
+    YamlMatrix im = loadImage(p);
+    CHECK(im.rows == 1 && im.cols == 2 && im.channels == 3 && im.dt == 'u');
+    CHECK(im.data.back() == 255.0);
+    bool threw = false;
+    try { readYamlMatrix(p, "missing"); } catch (const Error&) { threw = true; }
+    CHECK(threw);
+    // round trip through saveImage
+    YamlMatrix m;
+    m.rows = 3; m.cols = 4; m.dt = 'd';
+    std::mt19937 rng(3);
+    std::normal_distribution<double> nd;
+    for (int i = 0; i < 12; i++) m.data.push_back(nd(rng));
+    m.data[5] = HUGE_VAL;
+    const std::string q = dir + "/sva_test_image.yml";
+    saveImage(q, m);
+    YamlMatrix back = loadImage(q);
+    CHECK(back.rows == 3 && back.cols == 4 && back.dt == 'd' && back.data == m.data);
+    std::remove(p.c_str());
+    std::remove(q.c_str());
+}
+
 static void cpu_tests() {
+    yaml_tests();
     auto cams = rig(640);
     // getCameraPairs (functions.cpp:148-197)
     CHECK(getCameraPairs(cams, MID_LEFT) == (std::vector<std::array<int, 2>>{{12, 11}}));
@@ -196,6 +234,18 @@ static void gpu_tests() {
     CHECK(hw == W / 2 && hh == H / 2 && half.size() == (size_t)hw * hh);
     const int s4 = imgs[0][0] + imgs[0][1] + imgs[0][W] + imgs[0][W + 1];
     CHECK(half[0] == (uint8_t)((s4 + 2) >> 2));
+
+    // evaluation (CameraStereoVision.cpp:107-110; functions.cpp:348-354)
+    const std::vector<double> row = {0.0, 10.0};
+    CHECK(resizeLinear(eng, row, 2, 1, 4, 1) == (std::vector<double>{0.0, 2.5, 7.5, 10.0}));
+    YamlMatrix ref;
+    ref.rows = 1; ref.cols = 4; ref.dt = 'd';
+    ref.data = {0.0, 2.0, 7.0, 10.0};
+    CHECK(refError(eng, row, 2, 1, ref) == (std::vector<double>{0.0, 25.0, 25.0, 0.0}));
+    const std::vector<double> img = {1.0, 2.0, 3.0, 4.0};
+    const std::vector<uint8_t> msk = {1, 0, 1, 0};
+    CHECK(calculateAverageError(eng, img, 2, 2, &msk) == 2.0);
+    CHECK(calculateAverageError(eng, img, 2, 2) == 2.5);
 }
 
 int main(int argc, char** argv) {
