@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""SURVEY.md §8f rows 1-2 throughput on the GPU vs the CPU oracle (1 thread):
-improveWithDisparity (4 CROSS pairs of camera 12, 20x20 windows, a centred
-face-sized mask), shiftPerspective2, Points3DToDepthMap and DepthMapToPoints3D
-at 1920x1080, inputs resident in HBM (device entry points), hipEvent kernel
-times.  One JSON line per routine."""
+"""SURVEY.md §8f rows 1-4 throughput on the GPU vs the CPU oracle (1 thread),
+at 1920x1080 with inputs resident in HBM (device entry points) and hipEvent
+kernel times; one JSON line per routine:
+  improveWithDisparity (4 CROSS pairs of camera 12, 20x20 windows, a centred
+  face-sized mask, and without a mask), shiftPerspective2,
+  DepthMapToPoints3D, Points3DToDepthMap, the ingestion resize, and the
+  evaluation error map / masked mean."""
 import json
 import os
 import sys
@@ -137,6 +139,46 @@ def main():
                       "points": int(opts.shape[0]), "gpu_ms": round(dt * 1e3, 3),
                       "kernels_ms": ks, "cpu_ms_1thread": round(cdt * 1e3, 1),
                       "speedup": round(cdt / dt, 1)}), flush=True)
+
+    # ingestion: resize(img, img, Size(), 0.5, 0.5) of a 1080p u8 frame
+    img = synth.texture(H, W, 9)
+    d_img = torch.from_numpy(img).to(dev)
+    hw, hh = sva.resize_half_size(W, H)
+    d_half = torch.zeros((hh, hw), dtype=torch.uint8, device=dev)
+    dt, ks = timed(lambda: ctx.resize_half_d(d_img.data_ptr(), W, H, W, d_half.data_ptr(), hw),
+                   ["resize_half"])
+    t0 = time.perf_counter()
+    pyoracle.resize_half(img)
+    cdt = time.perf_counter() - t0
+    print(json.dumps({"routine": "resizeHalf", "size": f"{W}x{H}", "gpu_ms": round(dt * 1e3, 3),
+                      "kernels_ms": ks, "cpu_ms_1thread": round(cdt * 1e3, 1),
+                      "speedup": round(cdt / dt, 1)}), flush=True)
+
+    # evaluation: error map of a 960x540 depth against a 1080p reference, and
+    # the masked mean of that error (CameraStereoVision.cpp:107-110)
+    dep = rng.uniform(0.3, 2.0, size=(hh, hw))
+    refm = rng.uniform(0.3, 2.0, size=(H, W))
+    d_dep, d_ref = torch.from_numpy(dep).to(dev), torch.from_numpy(refm).to(dev)
+    d_err = torch.zeros((H, W), dtype=torch.float64, device=dev)
+    dt, ks = timed(lambda: ctx.ref_error_d(d_dep.data_ptr(), hw, hh, d_ref.data_ptr(), W, H, 50.0,
+                                           d_err.data_ptr()), ["resize_linear"])
+    t0 = time.perf_counter()
+    err = pyoracle.ref_error(dep, refm, 50.0)
+    cdt = time.perf_counter() - t0
+    print(json.dumps({"routine": "refError", "size": f"{hw}x{hh}->{W}x{H}",
+                      "gpu_ms": round(dt * 1e3, 3), "kernels_ms": ks,
+                      "cpu_ms_1thread": round(cdt * 1e3, 1), "speedup": round(cdt / dt, 1)}),
+          flush=True)
+    d_mask = torch.from_numpy(mask).to(dev)
+    dt, ks = timed(lambda: ctx.masked_mean_d(d_err.data_ptr(), d_mask.data_ptr(), W, H),
+                   ["masked_mean"])
+    t0 = time.perf_counter()
+    pyoracle.masked_mean(err, mask)
+    cdt = time.perf_counter() - t0
+    print(json.dumps({"routine": "calculateAverageError", "size": f"{W}x{H}",
+                      "gpu_ms_incl_sync": round(dt * 1e3, 3), "kernels_ms": ks,
+                      "cpu_ms_1thread": round(cdt * 1e3, 1), "speedup": round(cdt / dt, 1)}),
+          flush=True)
     ctx.close()
 
 
