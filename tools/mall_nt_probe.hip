@@ -70,6 +70,25 @@ int main() {
         std::printf("{\"table_MB\": 2048, \"stream_MB\": 0, \"nt\": 0, \"read_TBps\": %.2f}\n",
                     2048.0 * MB / (tot / 5 * 1e-3) / 1e12);
     }
+    // store-only rate: 256 MB and 1 GB streams, default and nt stores
+    for (int S : {256, 1024})
+        for (int nt = 0; nt < 2; nt++) {
+            const size_t m = (size_t)S * MB / 16;
+            write_kernel<<<grid, block>>>(x, m, nt);
+            CK(hipDeviceSynchronize());
+            float tot = 0;
+            for (int r = 0; r < 10; r++) {
+                CK(hipEventRecord(e0));
+                write_kernel<<<grid, block>>>(x, m, nt);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                tot += ms;
+            }
+            std::printf("{\"store_MB\": %d, \"nt\": %d, \"store_us\": %.2f, \"store_TBps\": %.2f}\n",
+                        S, nt, tot / 10 * 1e3, (double)S * MB / (tot / 10 * 1e-3) / 1e12);
+        }
     for (int T : tables)
         for (int nt = 0; nt < 2; nt++)
             for (int S : streams) {
