@@ -123,6 +123,11 @@ int sva_cost_d(void* ctx, const uint64_t* census_l, const uint64_t* census_r, in
                int height, const sva_sgm_params* p, uint8_t* C);
 int sva_paths_d(void* ctx, const uint8_t* C, int width, int height, const sva_sgm_params* p,
                 uint8_t* L8);
+/* The 8 path volumes straight from the two images through the census-fused
+ * path kernel (no cost volume; the kernel sva_disparity_sgm* runs for 1-D
+ * steps, dir_y = 0).  Same L8 layout and values as census -> cost -> paths. */
+int sva_paths_fused_d(void* ctx, const uint8_t* left, const uint8_t* right, int width,
+                      int height, size_t pitch, const sva_sgm_params* p, uint8_t* L8);
 int sva_aggregate_d(void* ctx, const uint8_t* C, int width, int height,
                     const sva_sgm_params* p, uint16_t* S);
 int sva_wta_d(void* ctx, const uint16_t* S, int width, int height, const sva_sgm_params* p,

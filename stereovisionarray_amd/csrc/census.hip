@@ -75,7 +75,8 @@ constexpr int LOADS = (TY * LW + TX * TY - 1) / (TX * TY);   // bytes per thread
 
 __global__ __launch_bounds__(TX* TY) void census9x7_rows_kernel(
     const uint8_t* __restrict__ img0, const uint8_t* __restrict__ img1, int W, int H,
-    size_t pitch, uint64_t* __restrict__ out0, uint64_t* __restrict__ out1, int rows) {
+    size_t pitch, uint64_t* __restrict__ out0, uint64_t* __restrict__ out1, int rows,
+    size_t ostride, int pr) {
     const uint8_t* __restrict__ img = blockIdx.z ? img1 : img0;
     uint64_t* __restrict__ out = blockIdx.z ? out1 : out0;
     __shared__ __attribute__((aligned(16))) uint8_t ring[RING][LW];   // LW = 72: rows dword-aligned
@@ -144,7 +145,11 @@ __global__ __launch_bounds__(TX* TY) void census9x7_rows_kernel(
                 }
                 word = ((uint64_t)hi << 32) | lo;
             }
-            out[(size_t)y * W + x] = word;
+            uint64_t* orow = out + (size_t)y * ostride;
+            orow[x] = word;
+            // padded layout (fused path): columns W .. W+pr-1
+            // repeat the row cyclically, orow[W + j] = orow[j mod W]
+            for (int cpad = x + W; cpad < W + pr; cpad += W) orow[cpad] = word;
         }
     }
 }
@@ -152,13 +157,15 @@ __global__ __launch_bounds__(TX* TY) void census9x7_rows_kernel(
 }  // namespace
 
 static hipError_t census_launch(Ctx& c, const uint8_t* a, const uint8_t* b, int W, int H,
-                                size_t pitch, uint64_t* oa, uint64_t* ob, int n) {
+                                size_t pitch, uint64_t* oa, uint64_t* ob, int n,
+                                size_t ostride = 0, int pr = 0) {
 #ifdef SVA_PATHS_ABLATION   // A/B builds only: SVA_CENSUS_VARIANT=1 selects the single-tile kernel
     static const int variant = getenv("SVA_CENSUS_VARIANT") ? atoi(getenv("SVA_CENSUS_VARIANT")) : 0;
 #else
     constexpr int variant = 0;
 #endif
-    if (variant == 1) {   // single-tile kernel
+    if (ostride == 0) ostride = (size_t)W;
+    if (variant == 1 && ostride == (size_t)W) {   // single-tile kernel
         dim3 grid((W + TX - 1) / TX, (H + TY - 1) / TY, n);
         hipLaunchKernelGGL(census9x7_kernel, grid, dim3(TX, TY), 0, c.stream, a, b, W, H, pitch,
                            oa, ob);
@@ -166,7 +173,7 @@ static hipError_t census_launch(Ctx& c, const uint8_t* a, const uint8_t* b, int 
     }
     dim3 grid((W + TX - 1) / TX, (H + kCensusRows - 1) / kCensusRows, n);
     hipLaunchKernelGGL(census9x7_rows_kernel, grid, dim3(TX, TY), 0, c.stream, a, b, W, H, pitch,
-                       oa, ob, kCensusRows);
+                       oa, ob, kCensusRows, ostride, pr);
     return hipGetLastError();
 }
 
@@ -180,6 +187,13 @@ hipError_t launch_census_pair(Ctx& c, const uint8_t* left, const uint8_t* right,
                               size_t pitch, uint64_t* out_l, uint64_t* out_r) {
     ScopedKernelTimer t(c, "census");
     return census_launch(c, left, right, W, H, pitch, out_l, out_r, 2);
+}
+
+hipError_t launch_census_pair_padded(Ctx& c, const uint8_t* left, const uint8_t* right, int W,
+                                     int H, size_t pitch, int pr, uint64_t* out_l,
+                                     uint64_t* out_r) {
+    ScopedKernelTimer t(c, "census");
+    return census_launch(c, left, right, W, H, pitch, out_l, out_r, 2, (size_t)W + pr, pr);
 }
 
 }  // namespace sva

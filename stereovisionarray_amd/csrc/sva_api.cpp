@@ -154,9 +154,62 @@ int check_sgm(Ctx* c, const sva_sgm_params* p, int W) {
     return SVA_OK;
 }
 
+// The census-fused path kernel (sgm_fused.hip) serves 1-D steps; array pairs on
+// 2-D steps (dir_y != 0) keep the materialised cost volume (cost2 + sgm_paths).
+bool use_fused(const sva_sgm_params* p, int W, int H) {
+#ifdef SVA_PATHS_ABLATION   // A/B builds only: SVA_FUSED=0 forces the cost-volume path
+    static const int on = getenv("SVA_FUSED") ? atoi(getenv("SVA_FUSED")) : 1;
+    if (!on) return false;
+#endif
+    return p->dir_y == 0 && fused_fits(W, H, p->D, p->dmin);
+}
+
+// Padded census pair for the fused path: one buffer [Lp | Rp], each map
+// H rows of W + pr words.  Returns the map size in words.
+int census_padded(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int H, size_t pitch,
+                  const sva_sgm_params* p, size_t* map_words) {
+    const int pr = fused_pad(W, p->D, p->dmin);
+    const size_t mw = (size_t)H * (size_t)(W + pr);
+    SVA_HIP(c, c->census_l.ensure(2 * mw * 8), "census workspace");
+    uint64_t* cen = (uint64_t*)c->census_l.ptr;
+    SVA_HIP(c, launch_census_pair_padded(*c, left, right, W, H, pitch, pr, cen, cen + mw),
+            "census launch");
+    *map_words = mw;
+    return SVA_OK;
+}
+
+int run_sgm_fused(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int H, size_t pitch,
+                  const sva_sgm_params* p, uint16_t* disp, float* sub) {
+    const size_t np = (size_t)W * H, nv = np * (size_t)p->D;
+    const int dir = p->dir > 0 ? 1 : -1;
+    SVA_HIP(c, c->paths.ensure(nv * 8), "path workspace");
+    uint8_t* L8 = (uint8_t*)c->paths.ptr;
+    size_t mw = 0;
+    int s = census_padded(c, left, right, W, H, pitch, p, &mw);
+    if (s) return s;
+    const uint64_t* cen = (const uint64_t*)c->census_l.ptr;
+    SVA_HIP(c, launch_paths_fused(*c, cen, 2 * mw, 0, mw, W, H, p->D, p->dmin, dir, p->P1, p->P2,
+                                  L8),
+            "paths launch");
+    SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, disp, sub), "wta launch");
+    if (p->lr_check) {
+        SVA_HIP(c, c->disp_r.ensure(np * 2), "lr workspace");
+        uint16_t* dr = (uint16_t*)c->disp_r.ptr;
+        // right image as reference: the census maps swap roles, the step flips
+        SVA_HIP(c, launch_paths_fused(*c, cen, 2 * mw, mw, 0, W, H, p->D, p->dmin, -dir, p->P1,
+                                      p->P2, L8),
+                "paths launch");
+        SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, dr, nullptr), "wta launch");
+        SVA_HIP(c, launch_lr_check(*c, disp, dr, W, H, dir, 0, p->lr_max_diff, p->invalid),
+                "lr launch");
+    }
+    return SVA_OK;
+}
+
 // Mode S on device buffers: census -> cost -> 8 paths -> WTA (-> L/R check).
 int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int H, size_t pitch,
                    const sva_sgm_params* p, uint16_t* disp, float* sub) {
+    if (use_fused(p, W, H)) return run_sgm_fused(c, left, right, W, H, pitch, p, disp, sub);
     const size_t np = (size_t)W * H, nv = np * (size_t)p->D;
     SVA_HIP(c, c->census_l.ensure(np * 8), "census workspace");
     SVA_HIP(c, c->census_r.ensure(np * 8), "census workspace");
@@ -366,7 +419,8 @@ int sva_reserve(void* ctx, int W, int H, int D) {
     SVA_CHECK_CTX(c);
     if (W <= 0 || H <= 0 || D <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad reserve size");
     const size_t np = (size_t)W * H, nv = np * (size_t)D;
-    SVA_HIP(c, c->census_l.ensure(np * 16), "reserve");
+    // padded census pair of the fused path at dmin = 0 (grows if a call needs more)
+    SVA_HIP(c, c->census_l.ensure(2 * (size_t)H * (size_t)(W + fused_pad(W, D, 0)) * 8), "reserve");
     SVA_HIP(c, c->census_r.ensure(np * 8), "reserve");
     SVA_HIP(c, c->cost.ensure(nv), "reserve");
     SVA_HIP(c, c->paths.ensure(nv * 8), "reserve");
@@ -473,6 +527,25 @@ int sva_paths_d(void* ctx, const uint8_t* C, int W, int H, const sva_sgm_params*
     if ((s = check_sgm(c, p, W))) return s;
     if (!C || !L8 || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
     SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
+    return SVA_OK;
+}
+
+int sva_paths_fused_d(void* ctx, const uint8_t* left, const uint8_t* right, int W, int H,
+                      size_t pitch, const sva_sgm_params* p, uint8_t* L8) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_image(c, left, W, H, pitch)) || (s = check_image(c, right, W, H, pitch)) ||
+        (s = check_sgm(c, p, W)))
+        return s;
+    if (!L8) return fail(c, SVA_ERR_INVALID_ARG, "null path volume output");
+    if (p->dir_y != 0 || !fused_fits(W, H, p->D, p->dmin))
+        return fail(c, SVA_ERR_UNSUPPORTED, "fused path: 1-D steps (dir_y = 0) only");
+    size_t mw = 0;
+    if ((s = census_padded(c, left, right, W, H, pitch, p, &mw))) return s;
+    SVA_HIP(c, launch_paths_fused(*c, (const uint64_t*)c->census_l.ptr, 2 * mw, 0, mw, W, H, p->D,
+                                  p->dmin, p->dir > 0 ? 1 : -1, p->P1, p->P2, L8),
+            "paths launch");
     return SVA_OK;
 }
 

@@ -81,6 +81,11 @@ struct ScopedKernelTimer {
 hipError_t launch_census(Ctx& c, const uint8_t* img, int W, int H, size_t pitch, uint64_t* out);
 hipError_t launch_census_pair(Ctx& c, const uint8_t* left, const uint8_t* right, int W, int H,
                               size_t pitch, uint64_t* out_l, uint64_t* out_r);
+// Census pair into the padded layout of the fused path: row
+// stride W + pr words, columns W .. W+pr-1 repeat the row cyclically.
+hipError_t launch_census_pair_padded(Ctx& c, const uint8_t* left, const uint8_t* right, int W,
+                                     int H, size_t pitch, int pr, uint64_t* out_l,
+                                     uint64_t* out_r);
 // cost.hip
 hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,
                        int dmin, int dir, uint8_t* C);
@@ -88,6 +93,14 @@ hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, in
 hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
                         uint8_t* L8);
 bool paths_supported(int D);
+// sgm_fused.hip -- the same 8 path volumes computed straight from the census
+// maps (1-D steps, dir = +-1), no cost volume.  cen = padded census buffer,
+// map_l / map_r = word offsets of the reference / matched map inside it.
+int fused_pad(int W, int D, int dmin);
+bool fused_fits(int W, int H, int D, int dmin);
+hipError_t launch_paths_fused(Ctx& c, const uint64_t* cen, size_t cen_words, size_t map_l,
+                              size_t map_r, int W, int H, int D, int dmin, int dir, int P1,
+                              int P2, uint8_t* L8);
 // wta.hip
 hipError_t launch_sum(Ctx& c, const uint8_t* L8, int W, int H, int D, uint16_t* S);
 hipError_t launch_wta_from_paths(Ctx& c, const uint8_t* L8, int W, int H, int D, int dmin,
