@@ -33,6 +33,8 @@
 //     tail words and the 4 CL words), stages it in a wave-private LDS slot and
 //     each lane reads its DPL words back.  Loads run PF steps ahead in a
 //     register ring, the LDS read of step t+1 overlaps step t's compute.
+#include <cstdlib>
+
 #include "sgm_common.h"
 
 namespace sva {
@@ -195,10 +197,20 @@ __device__ __forceinline__ void fused_h(rsrc_t rC, rsrc_t rL, const FusedGeom& g
 }
 
 // ------------------------------------------------------ vertical/diagonal --
+// A wave's 4 lines sit DPL columns apart (x_0 + DPL*l), so lane k of line l
+// needs window words DPL*(l + k) + i: for one i, every lane of the wave reads
+// one of 19 consecutive words of a DPL-way transposed window -- no LDS bank
+// conflicts (lines one column apart made every ds_read 4-way conflicted:
+// 83 % of the LDS cycles in SQ_LDS_BANK_CONFLICT).
+// LDS slot (per wave): window word w (w < D + 3*DPL) at (w % DPL)*SROW + w/DPL,
+// then the 4 CL words.
+constexpr int SROW = 20;   // >= 19 columns; 2*SROW*NWL spreads the write groups over the banks
+template <int DPL> constexpr int slot_words() { return DPL * SROW + 4; }
+
 template <int NWL>
 struct VLoad {
     uint2 a[NWL];   // window words lane*NWL .. +NWL-1
-    uint2 b;        // lanes 0-2: window words D..D+2; lanes 3-6: CL of line lane-3
+    uint2 b;        // lanes < 3*DPL: window word D + lane; next 4 lanes: CL of line lane-3*DPL
 };
 
 template <int NWL>
@@ -221,14 +233,15 @@ __device__ __forceinline__ VLoad<NWL> vload(rsrc_t r, unsigned o1, unsigned o2) 
 
 template <int DPL, int SD, bool DIAG, int PF>
 __device__ __forceinline__ void fused_vd(rsrc_t rC, rsrc_t rL, const FusedGeom& g,
-                                         uint2* __restrict__ stg, int rx, int ry, int i0, int l,
+                                         uint2* __restrict__ stg, int rx, int ry, int b, int l,
                                          int k, int lane) {
     constexpr int NP = DPL / 2, NW = DPL / 4, D = 16 * DPL, NWL = D / 64;
     static_assert(PF % 2 == 0, "word buffers alternate by step parity");
+    static_assert(DPL == 4 * NWL, "ld1 rows: lane%4 * NWL + j");
     const int W = g.W, H = g.H, dmin = g.dmin;
     const unsigned P1 = (unsigned)g.P1, P2 = (unsigned)g.P2;
     const int steps = H;
-    const int line = i0 + l;
+    const int line = b + DPL * l;
     const bool live = line < W;
     const int y0 = ry > 0 ? 0 : H - 1;
     const unsigned WD = (unsigned)W * (unsigned)D;
@@ -237,13 +250,14 @@ __device__ __forceinline__ void fused_vd(rsrc_t rC, rsrc_t rL, const FusedGeom& 
     cc.x = live ? line : 0;
     cc.off = ((unsigned)y0 * (unsigned)W + (unsigned)cc.x) * (unsigned)D + (unsigned)(k * DPL);
     const unsigned sstride = (unsigned)((ry * W + rx) * D);
-    // group window cursor: the window of line 0 starts at column x_0 + cofs;
-    // line l (x_0 + l, unwrapped) reads it from word l on.
+    // group window cursor: the window starts at column x_0 + cofs (x_0 = line
+    // 0's column); line l sits at x_0 + DPL*l, unwrapped (the census pad repeats
+    // the row, so a diagonal group straddling the wrap still reads one window)
     const int cofs = SD > 0 ? dmin : -(dmin + D - 1);
     const unsigned WB = (unsigned)W * 8u;
     const unsigned gstride = (unsigned)(ry * g.Wp + rx) * 8u;
-    int px = i0;
-    unsigned pofs = g.offR + ((unsigned)y0 * (unsigned)g.Wp + (unsigned)(i0 + cofs)) * 8u;
+    int px = b;
+    unsigned pofs = g.offR + ((unsigned)y0 * (unsigned)g.Wp + (unsigned)(b + cofs)) * 8u;
     auto gadv = [&]() {
         pofs += gstride;
         if constexpr (DIAG) {
@@ -252,19 +266,23 @@ __device__ __forceinline__ void fused_vd(rsrc_t rC, rsrc_t rL, const FusedGeom& 
             else if (px < 0) { px += W; pofs += WB; }
         }
     };
+    // load offsets relative to pofs, and LDS positions, per lane (constants)
     const unsigned k1 = (unsigned)(lane * NWL) * 8u;
-    const unsigned k2 = lane < 3 ? (unsigned)(D + lane) * 8u
-                      : lane < 7 ? (g.offL - g.offR) + (unsigned)(lane - 3 - cofs) * 8u
-                                 : (unsigned)D * 8u;
-    // LDS slot: words [0, D+3) window, [D+3, D+7) CL of lines 0..3
-    const int ro = SD > 0 ? l + k * DPL : l + D - DPL - k * DPL;
+    const int cl_lane = lane - 3 * DPL;
+    const bool w2 = lane < 3 * DPL + 4;
+    const unsigned k2 = lane < 3 * DPL ? (unsigned)(D + lane) * 8u
+                      : w2 ? (g.offL - g.offR) + (unsigned)(DPL * cl_lane - cofs) * 8u
+                           : (unsigned)D * 8u;
+    const int p1 = (lane & 3) * NWL * SROW + (lane >> 2);
+    const int p2 = lane < 3 * DPL ? (lane % DPL) * SROW + 16 + lane / DPL : DPL * SROW + cl_lane;
+    const int rb = SD > 0 ? l + k : (DPL - 1) * SROW + l + 15 - k;
     auto stage = [&](const VLoad<NWL>& v, uint2 (&wv)[DPL], uint2& cl) {
 #pragma unroll
-        for (int j = 0; j < NWL; j++) stg[lane * NWL + j] = v.a[j];
-        if (lane < 7) stg[D + lane] = v.b;
+        for (int j = 0; j < NWL; j++) stg[p1 + j * SROW] = v.a[j];
+        if (w2) stg[p2] = v.b;
 #pragma unroll
-        for (int i = 0; i < DPL; i++) wv[i] = stg[ro + i];
-        cl = stg[D + 3 + l];
+        for (int i = 0; i < DPL; i++) wv[i] = stg[SD > 0 ? rb + i * SROW : rb - i * SROW];
+        cl = stg[DPL * SROW + l];
     };
 
     VLoad<NWL> ring[PF];
@@ -298,11 +316,8 @@ __device__ __forceinline__ void fused_vd(rsrc_t rC, rsrc_t rL, const FusedGeom& 
         const uint2 cl = clb[cur];
         unsigned c[NP];
 #pragma unroll
-        for (int q = 0; q < NP; q++) {
-            const int i0w = SD > 0 ? 2 * q : DPL - 1 - 2 * q;
-            const int i1w = SD > 0 ? 2 * q + 1 : DPL - 2 - 2 * q;
-            c[q] = hd(cl, wbuf[cur][i0w]) | (hd(cl, wbuf[cur][i1w]) << 16);
-        }
+        for (int q = 0; q < NP; q++)
+            c[q] = hd(cl, wbuf[cur][2 * q]) | (hd(cl, wbuf[cur][2 * q + 1]) << 16);
         const int nin = inside_count<SD>(cc.x, W, dmin);
         if (__builtin_amdgcn_ballot_w64(nin < D)) {
             const int nv = nin - k * DPL;
@@ -330,20 +345,26 @@ __device__ __forceinline__ void fused_vd(rsrc_t rC, rsrc_t rL, const FusedGeom& 
     });
 }
 
+// Vertical/diagonal groups: blocks of 4*DPL consecutive lines hold DPL groups
+// (waves); group j of a block owns lines base + j + DPL*l, l = 0..3.
+template <int DPL> __host__ __device__ constexpr int vd_groups(int W) {
+    return (W + 4 * DPL - 1) / (4 * DPL) * DPL;
+}
+
 template <int DPL, int SD>
 __global__ __launch_bounds__(FBLOCK) void sgm_fused_kernel(const uint64_t* __restrict__ cen,
                                                            uint8_t* __restrict__ L8,
                                                            FusedGeom g) {
-    __shared__ uint2 stage[FBLOCK / 64][16 * DPL + 8];
-    int b = blockIdx.x, r, lb;
-    if (b < 2 * g.blk_h) {   // horizontal lines first (the longest), with priority
-        r = b / g.blk_h;
-        lb = b - r * g.blk_h;
+    __shared__ uint2 stage[FBLOCK / 64][slot_words<DPL>()];
+    int bi = blockIdx.x, r, lb;
+    if (bi < 2 * g.blk_h) {   // horizontal lines first (the longest), with priority
+        r = bi / g.blk_h;
+        lb = bi - r * g.blk_h;
         __builtin_amdgcn_s_setprio(1);
     } else {
-        b -= 2 * g.blk_h;
-        r = 2 + b / g.blk_w;
-        lb = b - (r - 2) * g.blk_w;
+        bi -= 2 * g.blk_h;
+        r = 2 + bi / g.blk_w;
+        lb = bi - (r - 2) * g.blk_w;
     }
     const int k = threadIdx.x & 15;
     const rsrc_t rC = make_rsrc(cen, g.cen_bytes);
@@ -358,21 +379,24 @@ __global__ __launch_bounds__(FBLOCK) void sgm_fused_kernel(const uint64_t* __res
     // vertical / diagonal: a wave's 4 lines share one staged window, so a
     // partially filled wave keeps its phantom lines (they load, never store)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int i0 = lb * FLINES + wave * 4;
-    if (i0 >= g.W) return;
+    const int grp = lb * (FBLOCK / 64) + wave;
+    if (grp >= vd_groups<DPL>(g.W)) return;
+    const int base = grp / DPL * (4 * DPL) + grp % DPL;
+    if (base >= g.W) return;
     int rx, ry;
     dir_of(r, rx, ry);
     constexpr int PF = fpf<DPL>();
-    if (r >= 4) fused_vd<DPL, SD, true, PF>(rC, rL, g, stage[wave], rx, ry, i0, lane >> 4, k, lane);
-    else fused_vd<DPL, SD, false, PF>(rC, rL, g, stage[wave], rx, ry, i0, lane >> 4, k, lane);
+    if (r >= 4) fused_vd<DPL, SD, true, PF>(rC, rL, g, stage[wave], rx, ry, base, lane >> 4, k, lane);
+    else fused_vd<DPL, SD, false, PF>(rC, rL, g, stage[wave], rx, ry, base, lane >> 4, k, lane);
 }
 
 }  // namespace
 
 int fused_pad(int W, int D, int dmin) {
-    const long long pr = (long long)dmin + D + 3;
-    const long long p = pr < W ? pr : W;
-    return (int)(p < 3 ? 3 : p);
+    // lines of a vertical/diagonal wave reach 3*DPL columns past x_0 (unwrapped);
+    // matched columns of wrapped lines reach min(W, dmin + D) further
+    const long long md = (long long)dmin + D;
+    return (int)(3 * (D / 16) + (md < W ? md : W));
 }
 
 bool fused_fits(int W, int H, int D, int dmin) {
@@ -387,7 +411,8 @@ hipError_t launch_paths_fused(Ctx& c, const uint64_t* cen, size_t cen_words, siz
                               size_t map_r, int W, int H, int D, int dmin, int dir, int P1,
                               int P2, uint8_t* L8) {
     ScopedKernelTimer t(c, "sgm_paths");
-    if (!fused_fits(W, H, D, dmin) || cen_words * 8 >= (1ull << 31)) return hipErrorInvalidValue;
+    if (!paths_supported(D) || !fused_fits(W, H, D, dmin) || cen_words * 8 >= (1ull << 31))
+        return hipErrorInvalidValue;
     FusedGeom g;
     g.W = W; g.H = H; g.dmin = dmin; g.P1 = P1; g.P2 = P2;
     g.Wp = W + fused_pad(W, D, dmin);
@@ -395,24 +420,33 @@ hipError_t launch_paths_fused(Ctx& c, const uint64_t* cen, size_t cen_words, siz
     g.offR = (unsigned)(map_r * 8);
     g.cen_bytes = (unsigned)(cen_words * 8);
     g.blk_h = (H + FLINES - 1) / FLINES;
-    g.blk_w = (W + FLINES - 1) / FLINES;
+    const int groups = D == 64 ? vd_groups<4>(W) : D == 128 ? vd_groups<8>(W)
+                     : D == 192 ? vd_groups<12>(W) : vd_groups<16>(W);
+    g.blk_w = (groups + FBLOCK / 64 - 1) / (FBLOCK / 64);
     g.vol = (unsigned)((size_t)W * H * D);
     dim3 grid(2 * g.blk_h + 6 * g.blk_w);
-#define SVA_FUSED_LAUNCH(DPL)                                                                  \
-    do {                                                                                       \
-        if (dir > 0)                                                                           \
-            hipLaunchKernelGGL((sgm_fused_kernel<DPL, 1>), grid, dim3(FBLOCK), 0, c.stream, cen, \
-                               L8, g);                                                         \
-        else                                                                                   \
-            hipLaunchKernelGGL((sgm_fused_kernel<DPL, -1>), grid, dim3(FBLOCK), 0, c.stream,   \
-                               cen, L8, g);                                                    \
+#ifdef SVA_PATHS_ABLATION   // A/B builds only: SVA_FUSED_KIND 1 = horizontal lines only,
+                            // 2 = vertical + diagonal only
+    {
+        static const int kind = getenv("SVA_FUSED_KIND") ? atoi(getenv("SVA_FUSED_KIND")) : 0;
+        if (kind == 1) grid = dim3(2 * g.blk_h);
+        if (kind == 2) { g.blk_h = 0; grid = dim3(6 * g.blk_w); }
+    }
+#endif
+#define SVA_FUSED_LAUNCH(DPL)                                                                   \
+    do {                                                                                        \
+        if (dir > 0)                                                                            \
+            hipLaunchKernelGGL((sgm_fused_kernel<DPL, 1>), grid, dim3(FBLOCK), 0, c.stream, cen,  \
+                               L8, g);                                                          \
+        else                                                                                    \
+            hipLaunchKernelGGL((sgm_fused_kernel<DPL, -1>), grid, dim3(FBLOCK), 0, c.stream,    \
+                               cen, L8, g);                                                     \
     } while (0)
     switch (D) {
         case 64: SVA_FUSED_LAUNCH(4); break;
         case 128: SVA_FUSED_LAUNCH(8); break;
         case 192: SVA_FUSED_LAUNCH(12); break;
-        case 256: SVA_FUSED_LAUNCH(16); break;
-        default: return hipErrorInvalidValue;
+        default: SVA_FUSED_LAUNCH(16); break;
     }
 #undef SVA_FUSED_LAUNCH
     return hipGetLastError();

@@ -50,7 +50,7 @@ def check(ctx, sva, oracle, torch_dev, W, H, D, dmin, dir, seed, P1=10, P2=120, 
 
 @pytest.mark.parametrize("D", [64, 128, 192, 256])
 @pytest.mark.parametrize("dir", [-1, 1])
-@pytest.mark.parametrize("W,H,dmin", [(37, 23, 0), (23, 61, 3), (130, 41, 0), (203, 19, 17)])
+@pytest.mark.parametrize("W,H,dmin", [(37, 23, 0), (23, 61, 3), (130, 41, 0), (203, 19, 17), (33, 40, 1), (97, 9, 0)])
 def test_fused_volumes(ctx, sva, oracle, torch_dev, D, dir, W, H, dmin):
     """Ragged widths (partial waves, phantom lines), tall images (diagonal lines
     wrap in x more than once) and D > W (every pixel has outside disparities)."""
