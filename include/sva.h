@@ -97,6 +97,17 @@ const char* sva_status_string(int status);
 /* Pre-size the workspace for W x H x D (optional; calls grow it on demand). */
 int sva_reserve(void* ctx, int width, int height, int D);
 
+/* Path-aggregation kernel for 1-D steps (dir_y = 0) of sva_disparity_sgm*.
+ * COST_VOLUME (default): census -> W*H*D u8 cost volume -> 8-path kernel
+ *   reading it (16 B/disp of HBM traffic in the path kernel, the fastest single
+ *   frame).  FUSED: the path kernel forms the Hamming costs in registers from
+ *   the census maps (8 B/disp, no cost volume; more VALU per disparity), which
+ *   pays when frames overlap on several streams.  Results are
+ *   identical.  2-D array steps always use the cost volume. */
+#define SVA_PATH_KERNEL_COST_VOLUME 0
+#define SVA_PATH_KERNEL_FUSED 1
+int sva_set_path_kernel(void* ctx, int kernel);
+
 /* Kernel timing with hipEvents on the context stream (measurement only). */
 int sva_set_timing(void* ctx, int enable);
 int sva_reset_timing(void* ctx);

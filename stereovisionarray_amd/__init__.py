@@ -27,12 +27,14 @@ SVA_ERR_UNSUPPORTED = 2
 SVA_ERR_DEVICE = 3
 SVA_ERR_OUT_OF_MEMORY = 4
 SVA_ERR_NO_DEVICE = 5
+SVA_PATH_KERNEL_COST_VOLUME = 0
+SVA_PATH_KERNEL_FUSED = 1
 
 # Symbols declared in include/sva.h (checked by tests/test_abi.py).
 EXPORTED = [
     "sva_sgm_params_default", "sva_abi_version", "sva_device_count", "sva_create",
     "sva_destroy", "sva_set_stream", "sva_synchronize", "sva_last_error",
-    "sva_status_string", "sva_reserve", "sva_set_timing", "sva_reset_timing",
+    "sva_status_string", "sva_reserve", "sva_set_path_kernel", "sva_set_timing", "sva_reset_timing",
     "sva_kernel_time", "sva_disparity_sgm", "sva_disparity_sgm_d", "sva_census_d",
     "sva_cost_d", "sva_paths_d", "sva_paths_fused_d", "sva_aggregate_d", "sva_wta_d", "sva_disparity_ref",
     "sva_disparity_ref_d", "sva_ref_endpoints_d", "sva_disparity_to_depth_d",
@@ -118,6 +120,7 @@ def _load() -> ct.CDLL:
         "sva_last_error": (ct.c_char_p, [vp]),
         "sva_status_string": (ct.c_char_p, [i32]),
         "sva_reserve": (i32, [vp, i32, i32, i32]),
+        "sva_set_path_kernel": (i32, [vp, i32]),
         "sva_set_timing": (i32, [vp, i32]),
         "sva_reset_timing": (i32, [vp]),
         "sva_kernel_time": (i32, [vp, ct.c_char_p, P(dbl), P(ct.c_int64)]),
@@ -244,6 +247,9 @@ class Context:
 
     def reserve(self, W, H, D):
         self._chk(lib.sva_reserve(self.h, W, H, D))
+
+    def set_path_kernel(self, kernel: int):
+        self._chk(lib.sva_set_path_kernel(self.h, kernel))
 
     def set_timing(self, on: bool):
         self._chk(lib.sva_set_timing(self.h, 1 if on else 0))

@@ -189,5 +189,134 @@ __device__ __forceinline__ void dir_of(int r, int& rx, int& ry) {
     ry = T[r][1];
 }
 
+// Prefetch depth in steps, per line kind.  Horizontal lines are the longest
+// (W steps) and few (2H lines): once the vertical/diagonal lines drain they
+// run alone and latency-bound, so they get a deeper ring (their next steps
+// are contiguous bytes, and VGPRs are not what limits occupancy here: the
+// grid has ~3.3 waves per SIMD at 1080p).
+// Measured in-process A/B (tools/ab_paths.py, 1080p D=128, same buffers,
+// alternating builds): PF_H/PF_V 8/8 0.755-0.788 ms; 32/8 0.665; 32/12 0.661;
+// 28/8 0.664; 40/8 0.689 (181 VGPRs -> 2 waves/SIMD); 32/4 0.770.  Part of the
+// gain is the occupancy cap itself: 149 VGPRs -> 3 waves/SIMD, and 8/8 with
+// LDS forcing 3 workgroups/CU is 0.730 vs 0.788 -- fewer concurrent line
+// streams, better DRAM locality.
+// Per disparities-per-lane (D = 16*DPL) overrides: SVA_PF_H<DPL>/SVA_PF_V<DPL>.
+// Chosen by the same in-process A/B: D=64 (1080p) 40/12 0.372 ms vs 8/8 0.416;
+// D=192 24/8 0.996 vs 12/8 1.154; D=256 (4K) 12/8 stays best (16/8 equal,
+// 20/8 and 12/12 +3 %).
+#ifndef SVA_PF_H4
+#define SVA_PF_H4 40
+#endif
+#ifndef SVA_PF_V4
+#define SVA_PF_V4 12
+#endif
+#ifndef SVA_PF_H8
+#define SVA_PF_H8 32
+#endif
+#ifndef SVA_PF_V8
+#define SVA_PF_V8 12
+#endif
+#ifndef SVA_PF_H12
+#define SVA_PF_H12 24
+#endif
+#ifndef SVA_PF_V12
+#define SVA_PF_V12 8
+#endif
+#ifndef SVA_PF_H16
+#define SVA_PF_H16 12
+#endif
+#ifndef SVA_PF_V16
+#define SVA_PF_V16 8
+#endif
+template <int DPL> constexpr int pf_h() {
+    return DPL == 4 ? SVA_PF_H4 : DPL == 8 ? SVA_PF_H8 : DPL == 12 ? SVA_PF_H12 : SVA_PF_H16;
+}
+template <int DPL> constexpr int pf_v() {
+    return DPL == 4 ? SVA_PF_V4 : DPL == 8 ? SVA_PF_V8 : DPL == 12 ? SVA_PF_V12 : SVA_PF_V16;
+}
+
+// One path line over a materialised cost volume C.
+template <int DPL, bool DIAG, int VAR, int PF>
+__device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& g, int rx, int ry,
+                                          int line, int k) {
+    constexpr int NW = DPL / 4, NP = DPL / 2;
+    const int W = g.W, H = g.H, D = g.D;
+    const unsigned P1 = (unsigned)g.P1, P2 = (unsigned)g.P2;
+    const int steps = ry == 0 ? W : H;
+    const unsigned WD = (unsigned)W * (unsigned)D;
+    const unsigned stride = (unsigned)((ry * W + rx) * D);
+    int x0, y0;
+    if (ry == 0) { y0 = line; x0 = rx > 0 ? 0 : W - 1; }
+    else { y0 = ry > 0 ? 0 : H - 1; x0 = line; }
+    Cursor<DIAG> cc;
+    cc.x = x0;
+    cc.off = ((unsigned)y0 * (unsigned)W + (unsigned)x0) * (unsigned)D + (unsigned)(k * DPL);
+    // Prefetch cursor: runs PF steps ahead and may run past the line's end;
+    // those loads land in-range garbage or, past the volume, the buffer range
+    // check returns 0 -- never consumed either way.
+    Cursor<DIAG> pc = cc;
+
+    unsigned A[NP];
+#pragma unroll
+    for (int j = 0; j < NP; j++) A[j] = 0u;   // L(q) = 0, m = 0  =>  L = C
+    unsigned m = 0u;
+
+    Words<NW> ring[PF];
+#pragma unroll
+    for (int p = 0; p < PF; p++) {
+        if constexpr (VAR == 3 || VAR == 4) {
+#pragma unroll
+            for (int w = 0; w < NW; w++) ring[p].w[w] = (0x05030201u * (unsigned)(p + 1) + (unsigned)k) & 0x1f1f1f1fu;
+        } else {
+            ring[p] = bload<NW>(rC, pc.off);
+        }
+        pc.advance(rx, stride, W, WD);
+    }
+
+    // One step consumes ring slot p in place (loaded PF steps ago) and only
+    // then refills that slot with the load for step t+PF, so the old and new
+    // values never overlap and the slot keeps its registers: no copies, and
+    // every wait is for a load issued ~PF steps earlier.  (Refilling first
+    // made hipcc copy the whole ring at the loop head behind vmcnt(1..3).)
+    auto step = [&](int p, bool refill) {
+        unsigned cw[NW];
+#pragma unroll
+        for (int w = 0; w < NW; w++) cw[w] = ring[p].w[w];
+        unsigned ow[NW];
+        sgm_step<DPL>(cw, A, m, ow, P1, P2);
+        bstore<NW, VAR>(rL, cc.off, ow, g.store_aux);
+        const bool wrapped = cc.advance(rx, stride, W, WD);
+        if constexpr (DIAG) {
+            if (wrapped) {
+#pragma unroll
+                for (int j = 0; j < NP; j++) A[j] = 0u;
+                m = 0u;
+            }
+        }
+        if (refill) {
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (VAR == 3 || VAR == 4) {
+#pragma unroll
+                for (int w = 0; w < NW; w++) ring[p].w[w] = (cw[w] * 3u + (unsigned)p) & 0x1f1f1f1fu;
+            } else {
+                ring[p] = bload<NW>(rC, pc.off);
+            }
+            pc.advance(rx, stride, W, WD);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    int t = 0;
+    for (; t + PF <= steps; t += PF) {
+#pragma unroll
+        for (int p = 0; p < PF; p++) step(p, true);
+    }
+    // tail: fewer than PF steps left, all already in the ring
+#pragma unroll
+    for (int p = 0; p < PF; p++)
+        if (t + p < steps) step(p, false);
+}
+
+
 }  // namespace sgm
 }  // namespace sva

@@ -367,8 +367,10 @@ __global__ __launch_bounds__(FBLOCK) void sgm_fused_kernel(const uint64_t* __res
         lb = bi - (r - 2) * g.blk_w;
     }
     const int k = threadIdx.x & 15;
-    const rsrc_t rC = make_rsrc(cen, g.cen_bytes);
     const rsrc_t rL = make_rsrc(L8 + (size_t)r * g.vol, g.vol);
+    int rx, ry;
+    dir_of(r, rx, ry);
+    const rsrc_t rC = make_rsrc(cen, g.cen_bytes);
     if (r < 2) {
         const int line = lb * FLINES + (threadIdx.x >> 4);
         if (line >= g.H) return;   // horizontal lines are independent: the row leaves
@@ -383,8 +385,6 @@ __global__ __launch_bounds__(FBLOCK) void sgm_fused_kernel(const uint64_t* __res
     if (grp >= vd_groups<DPL>(g.W)) return;
     const int base = grp / DPL * (4 * DPL) + grp % DPL;
     if (base >= g.W) return;
-    int rx, ry;
-    dir_of(r, rx, ry);
     constexpr int PF = fpf<DPL>();
     if (r >= 4) fused_vd<DPL, SD, true, PF>(rC, rL, g, stage[wave], rx, ry, base, lane >> 4, k, lane);
     else fused_vd<DPL, SD, false, PF>(rC, rL, g, stage[wave], rx, ry, base, lane >> 4, k, lane);

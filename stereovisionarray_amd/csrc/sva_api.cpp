@@ -154,14 +154,12 @@ int check_sgm(Ctx* c, const sva_sgm_params* p, int W) {
     return SVA_OK;
 }
 
-// The census-fused path kernel (sgm_fused.hip) serves 1-D steps; array pairs on
-// 2-D steps (dir_y != 0) keep the materialised cost volume (cost2 + sgm_paths).
-bool use_fused(const sva_sgm_params* p, int W, int H) {
-#ifdef SVA_PATHS_ABLATION   // A/B builds only: SVA_FUSED=0 forces the cost-volume path
-    static const int on = getenv("SVA_FUSED") ? atoi(getenv("SVA_FUSED")) : 1;
-    if (!on) return false;
-#endif
-    return p->dir_y == 0 && fused_fits(W, H, p->D, p->dmin);
+// Path kernel selection (sva_set_path_kernel): the census-fused
+// kernel serves 1-D steps (dir_y = 0); array pairs on 2-D steps always use the
+// materialised cost volume (cost2 + sgm_paths).
+bool use_fused(const Ctx* c, const sva_sgm_params* p, int W, int H) {
+    return c->path_kernel == SVA_PATH_KERNEL_FUSED && p->dir_y == 0 &&
+           fused_fits(W, H, p->D, p->dmin);
 }
 
 // Padded census pair for the fused path: one buffer [Lp | Rp], each map
@@ -178,6 +176,15 @@ int census_padded(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int 
     return SVA_OK;
 }
 
+// The fused path kernel for one reference/matched role of the padded census pair.
+int fused_paths(Ctx* c, size_t mw, bool swap, int W, int H, const sva_sgm_params* p, int dir,
+                uint8_t* L8) {
+    SVA_HIP(c, launch_paths_fused(*c, (const uint64_t*)c->census_l.ptr, 2 * mw, swap ? mw : 0,
+                                  swap ? 0 : mw, W, H, p->D, p->dmin, dir, p->P1, p->P2, L8),
+            "paths launch");
+    return SVA_OK;
+}
+
 int run_sgm_fused(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int H, size_t pitch,
                   const sva_sgm_params* p, uint16_t* disp, float* sub) {
     const size_t np = (size_t)W * H, nv = np * (size_t)p->D;
@@ -187,18 +194,13 @@ int run_sgm_fused(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int 
     size_t mw = 0;
     int s = census_padded(c, left, right, W, H, pitch, p, &mw);
     if (s) return s;
-    const uint64_t* cen = (const uint64_t*)c->census_l.ptr;
-    SVA_HIP(c, launch_paths_fused(*c, cen, 2 * mw, 0, mw, W, H, p->D, p->dmin, dir, p->P1, p->P2,
-                                  L8),
-            "paths launch");
+    if ((s = fused_paths(c, mw, false, W, H, p, dir, L8))) return s;
     SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, disp, sub), "wta launch");
     if (p->lr_check) {
         SVA_HIP(c, c->disp_r.ensure(np * 2), "lr workspace");
         uint16_t* dr = (uint16_t*)c->disp_r.ptr;
         // right image as reference: the census maps swap roles, the step flips
-        SVA_HIP(c, launch_paths_fused(*c, cen, 2 * mw, mw, 0, W, H, p->D, p->dmin, -dir, p->P1,
-                                      p->P2, L8),
-                "paths launch");
+        if ((s = fused_paths(c, mw, true, W, H, p, -dir, L8))) return s;
         SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, dr, nullptr), "wta launch");
         SVA_HIP(c, launch_lr_check(*c, disp, dr, W, H, dir, 0, p->lr_max_diff, p->invalid),
                 "lr launch");
@@ -209,7 +211,7 @@ int run_sgm_fused(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int 
 // Mode S on device buffers: census -> cost -> 8 paths -> WTA (-> L/R check).
 int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int H, size_t pitch,
                    const sva_sgm_params* p, uint16_t* disp, float* sub) {
-    if (use_fused(p, W, H)) return run_sgm_fused(c, left, right, W, H, pitch, p, disp, sub);
+    if (use_fused(c, p, W, H)) return run_sgm_fused(c, left, right, W, H, pitch, p, disp, sub);
     const size_t np = (size_t)W * H, nv = np * (size_t)p->D;
     SVA_HIP(c, c->census_l.ensure(np * 8), "census workspace");
     SVA_HIP(c, c->census_r.ensure(np * 8), "census workspace");
@@ -427,6 +429,15 @@ int sva_reserve(void* ctx, int W, int H, int D) {
     return SVA_OK;
 }
 
+int sva_set_path_kernel(void* ctx, int kernel) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    if (kernel != SVA_PATH_KERNEL_COST_VOLUME && kernel != SVA_PATH_KERNEL_FUSED)
+        return fail(c, SVA_ERR_INVALID_ARG, "unknown path kernel");
+    c->path_kernel = kernel;
+    return SVA_OK;
+}
+
 int sva_set_timing(void* ctx, int enable) {
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
@@ -543,9 +554,7 @@ int sva_paths_fused_d(void* ctx, const uint8_t* left, const uint8_t* right, int 
         return fail(c, SVA_ERR_UNSUPPORTED, "fused path: 1-D steps (dir_y = 0) only");
     size_t mw = 0;
     if ((s = census_padded(c, left, right, W, H, pitch, p, &mw))) return s;
-    SVA_HIP(c, launch_paths_fused(*c, (const uint64_t*)c->census_l.ptr, 2 * mw, 0, mw, W, H, p->D,
-                                  p->dmin, p->dir > 0 ? 1 : -1, p->P1, p->P2, L8),
-            "paths launch");
+    if ((s = fused_paths(c, mw, false, W, H, p, p->dir > 0 ? 1 : -1, L8))) return s;
     return SVA_OK;
 }
 

@@ -106,16 +106,23 @@ def test_reserve_timing_and_errors(ctx, sva):
     ctx.disparity_sgm(L, R, sva.default_params(D=128))
     ctx.disparity_sgm(L, R, sva.default_params(D=128))
     ctx.set_timing(False)
-    for name in ("census", "sgm_paths", "wta"):
+    for name in ("census", "cost", "sgm_paths", "wta"):
         ms, n = ctx.kernel_time(name)
         assert n == 2 and ms > 0.0, name
-    # 1-D steps run the census-fused path kernel: no cost volume, no cost kernel
-    assert ctx.kernel_time("cost") == (0.0, 0)
+    # the census-fused path kernel has no cost volume and no cost kernel
+    ctx.reset_timing()
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_FUSED)
     ctx.set_timing(True)
-    ctx.disparity_sgm(L, R, sva.default_params(D=128, dir=-1, dir_y=-1))   # 2-D step
-    ctx.set_timing(False)
-    ms, n = ctx.kernel_time("cost")
-    assert n == 1 and ms > 0.0
+    try:
+        ctx.disparity_sgm(L, R, sva.default_params(D=128))
+    finally:
+        ctx.set_timing(False)
+        ctx.set_path_kernel(sva.SVA_PATH_KERNEL_COST_VOLUME)
+    assert ctx.kernel_time("cost") == (0.0, 0)
+    assert ctx.kernel_time("sgm_paths")[1] == 1
+    with pytest.raises(sva.SvaError) as e:
+        ctx.set_path_kernel(7)
+    assert e.value.status == sva.SVA_ERR_INVALID_ARG
     assert ctx.kernel_time("no_such_kernel") == (0.0, 0)
     ctx.reset_timing()
     assert ctx.kernel_time("sgm_paths") == (0.0, 0)

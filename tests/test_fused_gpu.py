@@ -113,3 +113,59 @@ def test_fused_rejects_2d_step(ctx, sva, torch_dev):
     with pytest.raises(sva.SvaError) as e:
         ctx.paths_fused_d(L.data_ptr(), L.data_ptr(), 16, 16, 16, p, L8.data_ptr())
     assert e.value.status == sva.SVA_ERR_UNSUPPORTED
+
+
+@pytest.fixture
+def fused_ctx(ctx, sva):
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_FUSED)
+    yield ctx
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_COST_VOLUME)
+
+
+@pytest.mark.parametrize("W,H,D,dmin,dir", [
+    (160, 120, 64, 0, -1), (97, 61, 128, 3, 1), (256, 64, 192, 0, -1), (300, 70, 256, 5, 1),
+    (640, 480, 64, 44, 1),
+])
+def test_fused_pipeline(fused_ctx, sva, oracle, W, H, D, dmin, dir):
+    """sva_disparity_sgm on the fused path kernel: bit-exact disparities,
+    sub-pixel within the stated 1e-5 px."""
+    L, R, _ = synth.stereo_pair(H, W, D, dmin, dir, seed=W + D)
+    p = sva.default_params(D=D, dmin=dmin, dir=dir, subpixel=1)
+    disp, sub = fused_ctx.disparity_sgm(L, R, p)
+    od, osub = oracle.sgm(L, R, D, dmin, dir, subpixel=True, threads=8)
+    assert np.array_equal(disp, od)
+    assert np.max(np.abs(sub - osub)) <= 1e-5
+
+
+def test_fused_pipeline_lr_check(fused_ctx, sva, oracle):
+    """The L/R pass swaps the padded census maps' roles inside one buffer."""
+    W, H, D = 180, 60, 64
+    L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=11, stripes=6, step=9)
+    p = sva.default_params(D=D, lr_check=1, lr_max_diff=1, invalid=0xFFFF)
+    disp, _ = fused_ctx.disparity_sgm(L, R, p)
+    dl, _ = oracle.sgm(L, R, D, 0, -1, subpixel=False, threads=8)
+    dr, _ = oracle.sgm(R, L, D, 0, 1, subpixel=False, threads=8)
+    assert np.array_equal(disp, oracle.lr_check(dl, dr, -1, 1, 0xFFFF))
+
+
+def test_fused_pipeline_2d_step_uses_cost_volume(fused_ctx, sva, oracle):
+    """Array pairs on 2-D steps keep the cost-volume kernels in fused mode."""
+    A, B, _ = synth.stereo_pair2(90, 100, 64, 0, -2, -1, seed=5, stripes=4, step=8)
+    d, _ = fused_ctx.disparity_sgm(A, B, sva.default_params(D=64, dir=-2, dir_y=-1))
+    o, _ = oracle.sgm2(A, B, 64, 0, -2, -1, subpixel=False)
+    assert np.array_equal(d, o)
+
+
+@pytest.mark.slow
+def test_fused_full_size_1080p_d128(fused_ctx, sva):
+    """BASELINE config 2 at full size: fused and cost-volume kernels agree on
+    every disparity and sub-pixel value (the cost-volume path is checked against
+    the oracle at this size in test_sgm_gpu.py)."""
+    W, H, D = 1920, 1080, 128
+    L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=1)
+    p = sva.default_params(D=D, subpixel=1)
+    a, sa = fused_ctx.disparity_sgm(L, R, p)
+    fused_ctx.set_path_kernel(sva.SVA_PATH_KERNEL_COST_VOLUME)
+    b, sb = fused_ctx.disparity_sgm(L, R, p)
+    assert np.array_equal(a, b)
+    assert np.array_equal(sa.view(np.uint32), sb.view(np.uint32))

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--H", type=int, default=1080)
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--iters", type=int, default=30)
-    ap.add_argument("--entry", default="paths", choices=["paths", "sgm", "cost"])
+    ap.add_argument("--entry", default="paths", choices=["paths", "sgm", "cost", "fused"])
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -73,6 +73,10 @@ def main():
             if a.entry == "paths":
                 st = lib.sva_paths_d(h, ct.c_void_p(C.data_ptr()), W, H, ct.byref(p),
                                      ct.c_void_p(L8.data_ptr()))
+            elif a.entry == "fused":
+                st = lib.sva_paths_fused_d(h, ct.c_void_p(dL.data_ptr()), ct.c_void_p(dR.data_ptr()),
+                                           W, H, ct.c_size_t(W), ct.byref(p),
+                                           ct.c_void_p(L8.data_ptr()))
             elif a.entry == "cost":
                 st = lib.sva_cost_d(h, ct.c_void_p(cl.data_ptr()), ct.c_void_p(cr.data_ptr()), W, H,
                                     ct.byref(p), ct.c_void_p(C.data_ptr()))
@@ -92,6 +96,14 @@ def main():
                                ct.byref(p), ct.c_void_p(C.data_ptr()))
                 torch.cuda.synchronize()
                 outs.append(torch.sum(C.view(torch.int64)).item())
+            assert len(set(outs)) == 1, outs
+        if a.entry == "fused" and it == 0:
+            outs = []
+            for n, lib, h in handles:
+                lib.sva_paths_fused_d(h, ct.c_void_p(dL.data_ptr()), ct.c_void_p(dR.data_ptr()), W, H,
+                                      ct.c_size_t(W), ct.byref(p), ct.c_void_p(L8.data_ptr()))
+                torch.cuda.synchronize()
+                outs.append(torch.sum(L8.view(torch.int64)).item())
             assert len(set(outs)) == 1, outs
         if a.entry == "paths" and it == 0:
             # every variant must produce the same volumes
