@@ -186,14 +186,14 @@ __device__ __forceinline__ void fused_h(rsrc_t rC, rsrc_t rL, const FusedGeom& g
         soff += sstride;
     };
 
+    // one unrolled copy with a scalar guard per step (no separate tail copy:
+    // the hot code of all line kinds has to share the instruction cache)
     const int steps = W;
-    int t0 = 0;
-    for (; t0 + U <= steps; t0 += U) {
-        for_seq<U>([&](auto S) { step(S, t0 + S); });
+    for (int t0 = 0; t0 < steps; t0 += U) {
+        for_seq<U>([&](auto S) {
+            if (t0 + S < steps) step(S, t0 + S);
+        });
     }
-    for_seq<U>([&](auto S) {
-        if (t0 + S < steps) step(S, t0 + S);
-    });
 }
 
 // ------------------------------------------------------ vertical/diagonal --

@@ -1,0 +1,8 @@
+#!/bin/bash
+# experiment: fused parity per variant library (SVA_LIB_PATH)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+for l in ${LIBS}; do
+  SVA_LIB_PATH=$PWD/$l timeout -k 10 300 python -u -m pytest tests/test_fused_gpu.py -q --timeout 120 --timeout-method thread -k "volumes or tiny" > gpurun_out/fv.log 2>&1; rc=$?
+  echo "$l rc=$rc $(tail -1 gpurun_out/fv.log)"; grep -m3 "AssertionError: direction" gpurun_out/fv.log
+done
