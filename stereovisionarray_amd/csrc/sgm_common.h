@@ -286,12 +286,10 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
         sgm_step<DPL>(cw, A, m, ow, P1, P2);
         bstore<NW, VAR>(rL, cc.off, ow, g.store_aux);
         const bool wrapped = cc.advance(rx, stride, W, WD);
-        if constexpr (DIAG) {
-            if (wrapped) {
+        if constexpr (DIAG) {   // restart where x wraps: selects, no divergent branch
 #pragma unroll
-                for (int j = 0; j < NP; j++) A[j] = 0u;
-                m = 0u;
-            }
+            for (int j = 0; j < NP; j++) A[j] = wrapped ? 0u : A[j];
+            m = wrapped ? 0u : m;
         }
         if (refill) {
             __builtin_amdgcn_sched_barrier(0);

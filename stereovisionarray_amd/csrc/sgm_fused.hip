@@ -205,7 +205,7 @@ __device__ __forceinline__ void fused_h(rsrc_t rC, rsrc_t rL, const FusedGeom& g
 // LDS slot (per wave): window word w (w < D + 3*DPL) at (w % DPL)*SROW + w/DPL,
 // then the 4 CL words.
 constexpr int SROW = 20;   // >= 19 columns; 2*SROW*NWL spreads the write groups over the banks
-template <int DPL> constexpr int slot_words() { return DPL * SROW + 4; }
+template <int DPL> constexpr int slot_words() { return DPL * SROW + 4 + 64; }
 
 template <int NWL>
 struct VLoad {
@@ -274,12 +274,15 @@ __device__ __forceinline__ void fused_vd(rsrc_t rC, rsrc_t rL, const FusedGeom& 
                       : w2 ? (g.offL - g.offR) + (unsigned)(DPL * cl_lane - cofs) * 8u
                            : (unsigned)D * 8u;
     const int p1 = (lane & 3) * NWL * SROW + (lane >> 2);
-    const int p2 = lane < 3 * DPL ? (lane % DPL) * SROW + 16 + lane / DPL : DPL * SROW + cl_lane;
+    // lanes past the 3*DPL + 4 useful ones write a private dummy word (no
+    // divergent branch in the step: DPP results need a full exec mask)
+    const int p2 = lane < 3 * DPL ? (lane % DPL) * SROW + 16 + lane / DPL
+                 : w2 ? DPL * SROW + cl_lane : DPL * SROW + 4 + lane;
     const int rb = SD > 0 ? l + k : (DPL - 1) * SROW + l + 15 - k;
     auto stage = [&](const VLoad<NWL>& v, uint2 (&wv)[DPL], uint2& cl) {
 #pragma unroll
         for (int j = 0; j < NWL; j++) stg[p1 + j * SROW] = v.a[j];
-        if (w2) stg[p2] = v.b;
+        stg[p2] = v.b;
 #pragma unroll
         for (int i = 0; i < DPL; i++) wv[i] = stg[SD > 0 ? rb + i * SROW : rb - i * SROW];
         cl = stg[DPL * SROW + l];
@@ -325,14 +328,12 @@ __device__ __forceinline__ void fused_vd(rsrc_t rC, rsrc_t rL, const FusedGeom& 
         }
         unsigned ow[NW];
         sgm_step_c<DPL>(c, A, m, ow, P1, P2);
-        if (live) bstore<NW, 0>(rL, cc.off, ow, 0);
+        bstore<NW, 0>(rL, live ? cc.off : g.vol, ow, 0);   // phantom line: past the range, dropped
         const bool wrapped = cc.advance(rx, sstride, W, WD);
         if constexpr (DIAG) {
-            if (wrapped) {
 #pragma unroll
-                for (int j = 0; j < NP; j++) A[j] = 0u;
-                m = 0u;
-            }
+            for (int j = 0; j < NP; j++) A[j] = wrapped ? 0u : A[j];
+            m = wrapped ? 0u : m;
         }
     };
 
