@@ -62,6 +62,13 @@ def parse():
     ap.add_argument("--pairs-per-rank", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=1)
+    ap.add_argument("--streams", type=int, default=0,
+                    help="pairs of a step go round-robin to this many contexts, each with its "
+                         "own HIP stream and workspaces, so pairs overlap (0 = auto: 2 when a "
+                         "rank has several pairs per step, else 1)")
+    ap.add_argument("--path-kernel", default="auto", choices=["auto", "cost_volume", "fused"],
+                    help="sva_set_path_kernel (DESIGN.md §4.5); auto = the library's choice on "
+                         "one stream (fused for D=256), fused when pairs overlap on streams")
     ap.add_argument("--no-overlap", action="store_true",
                     help="gather each step's maps synchronously on the compute stream")
     ap.add_argument("--rehearse-overlap", action="store_true",
@@ -227,7 +234,8 @@ def load_traffic(workload):
 
 def timed(a, step, world, dev, ctx):
     """W untimed steps, then exactly K steps between barrier + synchronize,
-    max over ranks."""
+    max over ranks.  ctx: one context or a list (kernel timing on all)."""
+    ctxs = ctx if isinstance(ctx, list) else [ctx]
     import torch
     import torch.distributed as dist
     for _ in range(a.warmup):
@@ -236,8 +244,9 @@ def timed(a, step, world, dev, ctx):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ctx.set_timing(True)
-    ctx.reset_timing()
+    for c in ctxs:
+        c.set_timing(True)
+        c.reset_timing()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
@@ -246,7 +255,8 @@ def timed(a, step, world, dev, ctx):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    ctx.set_timing(False)
+    for c in ctxs:
+        c.set_timing(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device=dev if a.dist_backend == "nccl" else "cpu")
@@ -256,9 +266,15 @@ def timed(a, step, world, dev, ctx):
 
 
 def kernel_table(ctx, names=("census", "cost", "sgm_paths", "wta", "fuse_depth")):
+    """Average hipEvent duration per kernel, pooled over one or several contexts
+    (with --streams > 1 the launches overlap, so durations include contention)."""
+    ctxs = ctx if isinstance(ctx, list) else [ctx]
     kernels = {}
     for name in names:
-        ms, n = ctx.kernel_time(name)
+        ms = n = 0
+        for c in ctxs:
+            m1, n1 = c.kernel_time(name)
+            ms, n = ms + m1, n + n1
         if n:
             kernels[name] = {"avg_ms": ms / n, "launches": n}
     return kernels
@@ -442,11 +458,29 @@ def main():
             raise SystemExit("total_pairs must divide evenly over the ranks")
         P = wl["total_pairs"] // world
     params = sva.default_params(D=D, dmin=0, dir=-1, subpixel=1)
+    n_streams = a.streams if a.streams > 0 else (2 if P > 1 else 1)
+    path_kernel = a.path_kernel
+    if path_kernel == "auto" and n_streams > 1:
+        path_kernel = "fused"        # measured: fused + overlap beats both on one stream
+    kern = {"auto": sva.SVA_PATH_KERNEL_AUTO, "cost_volume": sva.SVA_PATH_KERNEL_COST_VOLUME,
+            "fused": sva.SVA_PATH_KERNEL_FUSED}[path_kernel]
     ctx = sva.Context(local)
     stream = torch.cuda.Stream(dev)     # non-default stream shared by kernels, copies, RCCL
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     ctx.reserve(W, H, D)
+    ctx.set_path_kernel(kern)
+    # --streams S: pair j of a step runs on context j % S (own stream and
+    # workspaces); the step's maps are complete once `stream` has waited on all
+    ctxs, cstreams = [ctx], [stream]
+    for _ in range(1, n_streams):
+        s_ = torch.cuda.Stream(dev)
+        c_ = sva.Context(local)
+        c_.set_stream(s_.cuda_stream)
+        c_.reserve(W, H, D)
+        c_.set_path_kernel(kern)
+        ctxs.append(c_)
+        cstreams.append(s_)
 
     n_units = world * P   # unit u = pair u, owned by rank u mod world (sdist.shard)
     seed0 = 0 if "total_pairs" in wl else 1   # config 5 seeds 0-255
@@ -479,9 +513,18 @@ def main():
         disp = disps[b]
         if gathered[b] is not None:      # the previous gather of this buffer is done
             stream.wait_event(gathered[b])
+        if len(ctxs) > 1:                # other streams start after this buffer is free
+            go = torch.cuda.Event()
+            go.record(stream)
+            for s_ in cstreams[1:]:
+                s_.wait_event(go)
         for j in range(P):
-            ctx.disparity_sgm_d(lefts[j].data_ptr(), rights[j].data_ptr(), W, H, W, params,
-                                disp[j].data_ptr(), sub[j].data_ptr())
+            ctxs[j % len(ctxs)].disparity_sgm_d(lefts[j].data_ptr(), rights[j].data_ptr(), W, H,
+                                                W, params, disp[j].data_ptr(), sub[j].data_ptr())
+        for s_ in cstreams[1:]:
+            done_ = torch.cuda.Event()
+            done_.record(s_)
+            stream.wait_event(done_)
         if world > 1 or comm is not None:   # the path's one exchange: maps -> rank 0 (RCCL)
             if a.dist_backend == "gloo" and world > 1:
                 sdist.gather_maps(disp.cpu(), n_units, dst=0)
@@ -498,8 +541,8 @@ def main():
                     ev.record(comm)
                     gathered[b] = ev
 
-    elapsed = timed(a, step, world, dev, ctx)
-    kernels = kernel_table(ctx)
+    elapsed = timed(a, step, world, dev, ctxs)
+    kernels = kernel_table(ctxs)
     # sanity: the result is a real disparity map (exact on the stripe interiors)
     d0 = disps[0][0].cpu().numpy().view(np.uint16)
     if rehearsal is not None and comm is not None:
@@ -530,7 +573,10 @@ def main():
                                f"WTA+subpixel), {P} pair(s)/rank",
                    "W": W, "H": H, "D": D, "P1": 10, "P2": 120,
                    "parallelism": f"pairs sharded over {world} rank(s), RCCL gather to rank 0"
-                                  + (" overlapped with the next step" if nbuf == 2 else "")},
+                                  + (" overlapped with the next step" if nbuf == 2 else ""),
+                   "streams_per_rank": len(ctxs),
+                   "path_kernel": path_kernel if path_kernel != "auto" else
+                   ("fused" if D == 256 else "cost_volume")},
         "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
         "roofline": roofline,
         "cpu_baseline": None,
@@ -546,7 +592,8 @@ def main():
             out["frame_overlap"] = frame_overlap_beside(W, H, D)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
 

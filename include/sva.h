@@ -98,14 +98,17 @@ const char* sva_status_string(int status);
 int sva_reserve(void* ctx, int width, int height, int D);
 
 /* Path-aggregation kernel for 1-D steps (dir_y = 0) of sva_disparity_sgm*.
- * COST_VOLUME (default): census -> W*H*D u8 cost volume -> 8-path kernel
- *   reading it (16 B/disp of HBM traffic in the path kernel, the fastest single
- *   frame).  FUSED: the path kernel forms the Hamming costs in registers from
- *   the census maps (8 B/disp, no cost volume; more VALU per disparity), which
- *   pays when frames overlap on several streams.  Results are
- *   identical.  2-D array steps always use the cost volume. */
+ * COST_VOLUME: census -> W*H*D u8 cost volume -> 8-path kernel reading it
+ *   (16 B/disp of HBM traffic in the path kernel).
+ * FUSED: the path kernel forms the Hamming costs in registers from the census
+ *   maps (8 B/disp, no cost volume, more VALU per disparity).
+ * AUTO (default): FUSED for D = 256, COST_VOLUME otherwise -- the faster one on
+ *   a single stream as measured on MI355X.  FUSED is also the
+ *   faster choice for any D when frames overlap on two streams.
+ * Results are identical.  2-D array steps always use the cost volume. */
 #define SVA_PATH_KERNEL_COST_VOLUME 0
 #define SVA_PATH_KERNEL_FUSED 1
+#define SVA_PATH_KERNEL_AUTO 2
 int sva_set_path_kernel(void* ctx, int kernel);
 
 /* Kernel timing with hipEvents on the context stream (measurement only). */

@@ -29,6 +29,7 @@ SVA_ERR_OUT_OF_MEMORY = 4
 SVA_ERR_NO_DEVICE = 5
 SVA_PATH_KERNEL_COST_VOLUME = 0
 SVA_PATH_KERNEL_FUSED = 1
+SVA_PATH_KERNEL_AUTO = 2
 
 # Symbols declared in include/sva.h (checked by tests/test_abi.py).
 EXPORTED = [

@@ -158,8 +158,9 @@ int check_sgm(Ctx* c, const sva_sgm_params* p, int W) {
 // kernel serves 1-D steps (dir_y = 0); array pairs on 2-D steps always use the
 // materialised cost volume (cost2 + sgm_paths).
 bool use_fused(const Ctx* c, const sva_sgm_params* p, int W, int H) {
-    return c->path_kernel == SVA_PATH_KERNEL_FUSED && p->dir_y == 0 &&
-           fused_fits(W, H, p->D, p->dmin);
+    const bool want = c->path_kernel == SVA_PATH_KERNEL_FUSED ||
+                      (c->path_kernel == SVA_PATH_KERNEL_AUTO && p->D == 256);
+    return want && p->dir_y == 0 && fused_fits(W, H, p->D, p->dmin);
 }
 
 // Padded census pair for the fused path: one buffer [Lp | Rp], each map
@@ -432,7 +433,8 @@ int sva_reserve(void* ctx, int W, int H, int D) {
 int sva_set_path_kernel(void* ctx, int kernel) {
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
-    if (kernel != SVA_PATH_KERNEL_COST_VOLUME && kernel != SVA_PATH_KERNEL_FUSED)
+    if (kernel != SVA_PATH_KERNEL_COST_VOLUME && kernel != SVA_PATH_KERNEL_FUSED &&
+        kernel != SVA_PATH_KERNEL_AUTO)
         return fail(c, SVA_ERR_INVALID_ARG, "unknown path kernel");
     c->path_kernel = kernel;
     return SVA_OK;

@@ -59,7 +59,7 @@ struct Ctx {
     // refinement / 3-D workspace (refine.hip)
     DevBuf in_c, shifted, keys, counts, total;
     int cu_count = 256;
-    int path_kernel = SVA_PATH_KERNEL_COST_VOLUME;   // sva_set_path_kernel
+    int path_kernel = SVA_PATH_KERNEL_AUTO;   // sva_set_path_kernel
 };
 
 // RAII helper: records timing events around one launch when enabled.

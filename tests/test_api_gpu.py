@@ -117,9 +117,24 @@ def test_reserve_timing_and_errors(ctx, sva):
         ctx.disparity_sgm(L, R, sva.default_params(D=128))
     finally:
         ctx.set_timing(False)
-        ctx.set_path_kernel(sva.SVA_PATH_KERNEL_COST_VOLUME)
+        ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
     assert ctx.kernel_time("cost") == (0.0, 0)
     assert ctx.kernel_time("sgm_paths")[1] == 1
+    # AUTO (the default) picks the fused kernel for D = 256 only
+    L2, R2, _ = synth.stereo_pair(64, 320, 256, 0, -1, seed=3)
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    ctx.disparity_sgm(L2, R2, sva.default_params(D=256))
+    ctx.set_timing(False)
+    assert ctx.kernel_time("cost") == (0.0, 0) and ctx.kernel_time("sgm_paths")[1] == 1
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_COST_VOLUME)
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    ctx.disparity_sgm(L2, R2, sva.default_params(D=256))
+    ctx.set_timing(False)
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
+    assert ctx.kernel_time("cost")[1] == 1
     with pytest.raises(sva.SvaError) as e:
         ctx.set_path_kernel(7)
     assert e.value.status == sva.SVA_ERR_INVALID_ARG

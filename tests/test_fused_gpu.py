@@ -119,7 +119,7 @@ def test_fused_rejects_2d_step(ctx, sva, torch_dev):
 def fused_ctx(ctx, sva):
     ctx.set_path_kernel(sva.SVA_PATH_KERNEL_FUSED)
     yield ctx
-    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_COST_VOLUME)
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
 
 
 @pytest.mark.parametrize("W,H,D,dmin,dir", [
@@ -167,5 +167,6 @@ def test_fused_full_size_1080p_d128(fused_ctx, sva):
     a, sa = fused_ctx.disparity_sgm(L, R, p)
     fused_ctx.set_path_kernel(sva.SVA_PATH_KERNEL_COST_VOLUME)
     b, sb = fused_ctx.disparity_sgm(L, R, p)
+    fused_ctx.set_path_kernel(sva.SVA_PATH_KERNEL_FUSED)
     assert np.array_equal(a, b)
     assert np.array_equal(sa.view(np.uint32), sb.view(np.uint32))

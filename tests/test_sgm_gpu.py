@@ -226,8 +226,16 @@ def test_full_size_4k_d256_properties(ctx, sva):
     R = np.zeros_like(L)
     R[:, : W - d0] = L[:, d0:]
     R[:, W - d0:] = synth.texture(H, d0, 4)
-    p = sva.default_params(D=D, dir=-1)
-    a, _ = ctx.disparity_sgm(L, R, p)
+    p = sva.default_params(D=D, dir=-1, subpixel=1)
+    a, sa = ctx.disparity_sgm(L, R, p)          # default AUTO: the fused kernel at D = 256
     b, _ = ctx.disparity_sgm(L, R, p)
     assert np.array_equal(a, b)
     assert (a[8:-8, d0 + 64: W - 64] == d0).all()
+    # the two path kernels agree on every disparity and sub-pixel value
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_COST_VOLUME)
+    try:
+        c, sc = ctx.disparity_sgm(L, R, p)
+    finally:
+        ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
+    assert np.array_equal(a, c)
+    assert np.array_equal(sa.view(np.uint32), sc.view(np.uint32))
