@@ -155,20 +155,30 @@ __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigne
     const unsigned Qlast = __builtin_amdgcn_alignbit(Y, A[NP - 1], 16);
     const unsigned mP2 = m + P2;
     const unsigned K = 0u - (m | (m << 16));
+    // Stage-major over the NP independent pairs, and a min TREE below: each
+    // packed op's result is consumed one pair later, not by the next
+    // instruction (gfx950 puts an s_nop between dependent VOP3P ops).
+    u16x2 t[NP];
 #pragma unroll
-    for (int j = 0; j < NP; j++) {
-        const u16x2 q = as_v2(j < NP - 1 ? M[j + 1] : Qlast);
-        u16x2 t = vmin2(as_v2(M[j]), q) + splat2(P1);
-        t = vmin2(t, as_v2(A[j]));
-        t = vmin2(t, splat2(mP2));
-        A[j] = add3(as_u32(t), c[j], K);
-    }
+    for (int j = 0; j < NP; j++) t[j] = vmin2(as_v2(M[j]), as_v2(j < NP - 1 ? M[j + 1] : Qlast));
+#pragma unroll
+    for (int j = 0; j < NP; j++) t[j] = t[j] + splat2(P1);
+#pragma unroll
+    for (int j = 0; j < NP; j++) t[j] = vmin2(t[j], as_v2(A[j]));
+#pragma unroll
+    for (int j = 0; j < NP; j++) t[j] = vmin2(t[j], splat2(mP2));
+#pragma unroll
+    for (int j = 0; j < NP; j++) A[j] = add3(as_u32(t[j]), c[j], K);
 #pragma unroll
     for (int w = 0; w < NW; w++) ow[w] = pack4(A[2 * w], A[2 * w + 1]);
-    u16x2 mm = as_v2(A[0]);
+    u16x2 mm[NP];
 #pragma unroll
-    for (int j = 1; j < NP; j++) mm = vmin2(mm, as_v2(A[j]));
-    m = row_min_u32(mm.x < mm.y ? mm.x : mm.y);
+    for (int j = 0; j < NP; j++) mm[j] = as_v2(A[j]);
+#pragma unroll
+    for (int s = 1; s < NP; s *= 2)
+#pragma unroll
+        for (int j = 0; j + s < NP; j += 2 * s) mm[j] = vmin2(mm[j], mm[j + s]);
+    m = row_min_u32(mm[0].x < mm[0].y ? mm[0].x : mm[0].y);
 }
 
 // The same step on u8-packed cost words (DPL/4 dwords of 4 disparities).

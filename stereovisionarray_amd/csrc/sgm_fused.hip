@@ -96,12 +96,16 @@ __device__ __forceinline__ uint2 bcast_row(uint2 v) {
 template <int NP>
 __device__ __forceinline__ void mask_outside(unsigned (&c)[NP], int nvalid) {
     const u16x2 nv = splat2((unsigned)nvalid);
+    u16x2 s[NP];
 #pragma unroll
     for (int j = 0; j < NP; j++) {
         const u16x2 dd = {(unsigned short)(2 * j + 1), (unsigned short)(2 * j + 2)};
-        const u16x2 s = __builtin_elementwise_sub_sat(dd, nv);
-        c[j] = as_u32(vmin2(s * splat2(62) + as_v2(c[j]), splat2(62)));
+        s[j] = __builtin_elementwise_sub_sat(dd, nv);
     }
+#pragma unroll
+    for (int j = 0; j < NP; j++) s[j] = s[j] * splat2(62) + as_v2(c[j]);
+#pragma unroll
+    for (int j = 0; j < NP; j++) c[j] = as_u32(vmin2(s[j], splat2(62)));
 }
 
 // Number of disparities d in [0, D) whose matched column x + SD*(dmin + d)
