@@ -256,6 +256,8 @@ public:
     void check(int s) const {
         if (s != SVA_OK) throw Error(s, sva_last_error(ctx_));
     }
+    // SVA_PATH_KERNEL_AUTO (default), _COST_VOLUME or _FUSED (sva.h)
+    void setPathKernel(int kernel) { check(sva_set_path_kernel(ctx_, kernel)); }
 
 private:
     void* ctx_ = nullptr;

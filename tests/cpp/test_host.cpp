@@ -162,6 +162,12 @@ static void gpu_tests() {
     std::vector<float> sub;
     auto ds = computeDisparitySGM(eng, views[12], views[13], p, &sub);
     CHECK(ds.size() == (size_t)W * H && sub.size() == ds.size());
+    // both path kernels give the same maps
+    std::vector<float> sub_f;
+    eng.setPathKernel(SVA_PATH_KERNEL_FUSED);
+    auto df = computeDisparitySGM(eng, views[12], views[13], p, &sub_f);
+    eng.setPathKernel(SVA_PATH_KERNEL_AUTO);
+    CHECK(df == ds && sub_f == sub);
     bool threw = false;
     try {
         p.D = 50;
