@@ -24,6 +24,8 @@ for step in "$@"; do
     array) run center8 600 python bench.py --workload center8 --steps 5 --warmup 2 --no-cpu-baseline
            run grid8_all 600 python bench.py --workload grid8_all --steps 5 --warmup 2 --no-cpu-baseline ;;
     batch) run batch256 900 python bench.py --workload batch256_d192 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    gloo2) run bench_gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo ;;
+    batch_gloo2) run batch_gloo2 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 --workload batch256_d192 --steps 1 --warmup 1 --dist-backend gloo ;;
     array_gloo2) run center8_gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --workload center8 --steps 3 --warmup 1 --dist-backend gloo ;;
     bench4k) run bench4k 600 python bench.py --steps 5 --warmup 2 --workload 4k_d256 --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
