@@ -7,15 +7,15 @@
 // is formed in registers from the two census maps instead of being read back
 // from a materialised W*H*D cost volume.  That removes the cost kernel's
 // 1 B/disp write and the 8 B/disp of cost re-reads (one per direction): the
-// path kernel's HBM traffic drops from 16 to 8 B/disp plus the census reads,
-// which the L2 serves (neighbouring lines share them).  The popcounts are
-// independent of the recurrence, so they fill the issue slots the dependent
-// DPP chain of the recurrence leaves idle (the v3 kernel
-// spends ~2x its issue time waiting on that chain).
+// path kernel's HBM traffic drops from 16 to 8 B/disp plus the census windows
+// (about half of them L2 hits).  The price is ~36 more VALU per lane-step at
+// D=128: on one stream this kernel wins at D=256 and loses at D<=192; with
+// frames overlapping on two streams it wins at every D (DESIGN.md §4.5,
+// sva_set_path_kernel).
 //
 // Census layout (census.hip, padded form): each map has row stride
 // Wp = W + pr words, and columns W .. W+pr-1 repeat the row cyclically.  The
-// pad is what lets a diagonal wave's four lines share one window when some of
+// pad is what lets a diagonal wave's lines share one window when some of
 // them have wrapped around x (see fused_vd).  Columns outside [0, W) are read
 // as whatever lies there (or 0 past the buffer: raw buffer loads are range
 // checked) and masked to 62 by mask_outside from the column arithmetic alone.
@@ -27,12 +27,16 @@
 //     row_newbcast of the entering word, which lane j of the line loaded for
 //     step 16q + j (one u64 load per lane per 16 steps, likewise for CL).
 //     The register slots rotate with the step (compile-time, no moves).
-//   * vertical / diagonal (H steps): the 4 lines of a wave sit on adjacent
-//     columns of one row, so their D-word windows overlap in D + 3 words.
-//     The wave loads that window once per step (D/64 words per lane, plus 3
-//     tail words and the 4 CL words), stages it in a wave-private LDS slot and
-//     each lane reads its DPL words back.  Loads run PF steps ahead in a
-//     register ring, the LDS read of step t+1 overlaps step t's compute.
+//   * vertical / diagonal (H steps): the 4 lines of a wave sit DPL columns
+//     apart, so their D-word windows overlap in D + 3*DPL words.  The wave
+//     loads that window once per step (D/64 words per lane, plus 3*DPL tail
+//     words and the 4 CL words), stages it DPL-way transposed in a
+//     wave-private LDS slot (conflict-free reads) and each lane reads its DPL
+//     words back.  Loads run PF steps ahead in a register ring, the LDS read
+//     of step t+1 overlaps step t's compute.
+//   * every step is branch-free apart from wave-uniform branches: the DPP
+//     neighbour exchange needs a full exec mask (a divergent store guard
+//     around it miscompiled under a guarded unroll).
 #include <cstdlib>
 
 #include "sgm_common.h"
