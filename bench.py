@@ -35,6 +35,8 @@ WORKLOADS = {
     "4k_d256": dict(W=3840, H=2160, D=256),      # BASELINE configs[2]
     "1080p_d192": dict(W=1920, H=1080, D=192),   # BASELINE configs[4] per-pair shape
     "vga_d64": dict(W=640, H=480, D=64),         # BASELINE configs[0] shape
+    "1080p_d64": dict(W=1920, H=1080, D=64),     # path-kernel selection sweep
+    "1080p_d256": dict(W=1920, H=1080, D=256),   # path-kernel selection sweep
     "1080half_d128": dict(W=1920, H=540, D=128), # experiment: C fits the Infinity Cache
     # BASELINE configs[3] as SURVEY.md §8d spells it: getCameraPairs(TO_CENTER_SMALL)
     # = 12 <-> {6,7,8,11,13,16,17,18} (functions.cpp:156-165), one pair per GPU at
