@@ -70,7 +70,10 @@ __global__ __launch_bounds__(TX* TY) void census9x7_kernel(const uint8_t* __rest
 // per step: ring slots are rewritten 4 steps after their rows were loaded and
 // 2 steps after their last reads (a step reads rows y-3 .. y+TY+2).
 constexpr int RING = 16;
-constexpr int kCensusRows = 32;
+#ifndef SVA_CENSUS_ROWS
+#define SVA_CENSUS_ROWS 16
+#endif
+constexpr int kCensusRows = SVA_CENSUS_ROWS;
 constexpr int LOADS = (TY * LW + TX * TY - 1) / (TX * TY);   // bytes per thread per step
 
 __global__ __launch_bounds__(TX* TY) void census9x7_rows_kernel(

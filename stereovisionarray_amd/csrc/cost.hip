@@ -177,7 +177,13 @@ __global__ __launch_bounds__(BLOCK) void hamming_cost2_kernel(
 // Tried and rejected: 64-pixel workgroups (2-4 passes over the 16-pixel
 // groups, less staging traffic per cost byte) -- cost-only A/B: D=128 -2.5 %,
 // D=64 equal, D=192 +22 %, D=256 (4K) +13 %.
-constexpr int kCostRows = 16;
+// Rows per workgroup.  Fewer rows = more workgroups in flight; measured
+// in-process (1080p, rows 1/2/4/16): D=64 0.038/0.033/0.032/0.033 ms, D=128
+// 0.072/0.067/0.072/0.079, D=192 0.115/0.099/0.104/0.113, D=256
+// 0.145/0.124/0.128/0.138; 4K D=256 0.61/0.52/0.50/0.49.
+__host__ __device__ constexpr int cost_rows(int W, int H, int D) {
+    return (D >= 128 && (long long)W * H <= 4000000ll) ? 2 : 4;
+}
 
 template <int NC>
 __global__ __launch_bounds__(256) void hamming_cost_rows_kernel(
@@ -304,7 +310,11 @@ hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, in
                            c.stream, cl, cr, W, H, D, dmin, dir, C);
         return hipGetLastError();
     }
-    const int rows = kCostRows;
+#ifdef SVA_COST_ROWS   // A/B builds only
+    const int rows = SVA_COST_ROWS;
+#else
+    const int rows = cost_rows(W, H, D);
+#endif
     // threads: 16 pixels x NC chunks per group, as many groups as fit 256
     const int nc = D / 16, groups = 256 / (16 * nc) > 0 ? 256 / (16 * nc) : 1;
     const int nt = groups * 16 * nc, px = groups * 16;

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--H", type=int, default=1080)
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--iters", type=int, default=30)
-    ap.add_argument("--entry", default="paths", choices=["paths", "sgm", "cost", "fused"])
+    ap.add_argument("--entry", default="paths", choices=["paths", "sgm", "cost", "fused", "census"])
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -73,6 +73,9 @@ def main():
             if a.entry == "paths":
                 st = lib.sva_paths_d(h, ct.c_void_p(C.data_ptr()), W, H, ct.byref(p),
                                      ct.c_void_p(L8.data_ptr()))
+            elif a.entry == "census":
+                st = lib.sva_census_d(h, ct.c_void_p(dL.data_ptr()), W, H, ct.c_size_t(W),
+                                      ct.c_void_p(cl.data_ptr()))
             elif a.entry == "fused":
                 st = lib.sva_paths_fused_d(h, ct.c_void_p(dL.data_ptr()), ct.c_void_p(dR.data_ptr()),
                                            W, H, ct.c_size_t(W), ct.byref(p),
