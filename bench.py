@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--rehearse-overlap", action="store_true",
                     help="N=1 only: run the overlapped-gather stream logic with a device copy "
                          "standing in for the RCCL gather (RCCL refuses 2 ranks on 1 GPU)")
+    ap.add_argument("--rehearse-rccl", action="store_true",
+                    help="N=1 only: a 1-rank RCCL process group runs the real overlapped "
+                         "gather_maps on the comm stream (the N>1 code path on one GPU)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (real runs); gloo = rehearsal with ranks "
                          "sharing one GPU, maps gathered through host memory")
@@ -247,7 +250,9 @@ def timed(a, step, world, dev, ctx):
         dist.barrier()
     torch.cuda.synchronize()
     for c in ctxs:
-        c.set_timing(True)
+        # only the roofline kernel is event-timed in the timed region: an event
+        # record costs a few us of stream time, 8 per frame cost ~2.5 %
+        c.set_timing(2)          # SVA_TIMING_PATHS
         c.reset_timing()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -265,6 +270,29 @@ def timed(a, step, world, dev, ctx):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
+
+
+def breakdown(a, step, world, ctx, timed_kernels):
+    """Per-kernel averages of every pipeline kernel from a short pass after the
+    timed region (all launches event-timed); sgm_paths keeps its timed-region
+    figure, which is the one the roofline uses."""
+    import torch
+    import torch.distributed as dist
+    ctxs = ctx if isinstance(ctx, list) else [ctx]
+    for c in ctxs:
+        c.set_timing(1)          # SVA_TIMING_ALL
+        c.reset_timing()
+    for _ in range(min(a.steps, 5)):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    kernels = kernel_table(ctxs)
+    for c in ctxs:
+        c.set_timing(0)
+    if "sgm_paths" in timed_kernels:
+        kernels["sgm_paths"] = timed_kernels["sgm_paths"]
+    return kernels
 
 
 def kernel_table(ctx, names=("census", "cost", "sgm_paths", "wta", "fuse_depth")):
@@ -373,7 +401,7 @@ def run_array(a, wl, world, rank, local, dev):
             maps["all"] = allm
 
     elapsed = timed(a, step, world, dev, ctx)
-    kernels = kernel_table(ctx)
+    kernels = breakdown(a, step, world, ctx, kernel_table(ctx))
     value = n_units * W * H * D * a.steps / elapsed / 1e6
     out = None
     if rank == 0:
@@ -443,6 +471,11 @@ def main():
     local = local % ndev if a.dist_backend == "gloo" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    rccl1 = world == 1 and a.rehearse_rccl
+    if rccl1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if a.dist_backend == "nccl":
@@ -494,7 +527,7 @@ def main():
     # Two map buffers: step i computes into buffer i%2 on the compute stream
     # while the gather of step i-1 (buffer (i-1)%2) runs on a comm stream.
     overlap = (world > 1 and a.dist_backend == "nccl" and not a.no_overlap) or \
-        (world == 1 and a.rehearse_overlap)
+        (world == 1 and (a.rehearse_overlap or rccl1))
     nbuf = 2 if overlap else 1
     disps = [torch.zeros((P, H, W), dtype=torch.int16, device=dev) for _ in range(nbuf)]
     sub = torch.zeros((P, H, W), dtype=torch.float32, device=dev)
@@ -506,6 +539,8 @@ def main():
     def gather(disp):
         if world > 1:
             sdist.gather_maps(disp, n_units, dst=0)
+        elif rccl1:                      # real RCCL gather in a 1-rank group
+            rehearsal[0].copy_(sdist.gather_maps(disp, n_units, dst=0))
         else:                            # --rehearse-overlap stand-in for the RCCL gather
             rehearsal[0].copy_(disp)
 
@@ -544,7 +579,7 @@ def main():
                     gathered[b] = ev
 
     elapsed = timed(a, step, world, dev, ctxs)
-    kernels = kernel_table(ctxs)
+    kernels = breakdown(a, step, world, ctxs, kernel_table(ctxs))
     # sanity: the result is a real disparity map (exact on the stripe interiors)
     d0 = disps[0][0].cpu().numpy().view(np.uint16)
     if rehearsal is not None and comm is not None:
@@ -596,7 +631,7 @@ def main():
         print(json.dumps(out), flush=True)
     for c in ctxs:
         c.close()
-    if world > 1:
+    if world > 1 or rccl1:
         dist.destroy_process_group()
 
 

@@ -111,7 +111,13 @@ int sva_reserve(void* ctx, int width, int height, int D);
 #define SVA_PATH_KERNEL_AUTO 2
 int sva_set_path_kernel(void* ctx, int kernel);
 
-/* Kernel timing with hipEvents on the context stream (measurement only). */
+/* Kernel timing with hipEvents on the context stream (measurement only).
+ * enable: SVA_TIMING_OFF, SVA_TIMING_ALL (every launch), or SVA_TIMING_PATHS
+ * (only the path-aggregation launch "sgm_paths": two event records per frame
+ * instead of eight; each record costs a few microseconds of stream time). */
+#define SVA_TIMING_OFF 0
+#define SVA_TIMING_ALL 1
+#define SVA_TIMING_PATHS 2
 int sva_set_timing(void* ctx, int enable);
 int sva_reset_timing(void* ctx);
 /* Total milliseconds and launch count of kernel `name` since the last reset. */

@@ -30,6 +30,9 @@ SVA_ERR_NO_DEVICE = 5
 SVA_PATH_KERNEL_COST_VOLUME = 0
 SVA_PATH_KERNEL_FUSED = 1
 SVA_PATH_KERNEL_AUTO = 2
+SVA_TIMING_OFF = 0
+SVA_TIMING_ALL = 1
+SVA_TIMING_PATHS = 2
 
 # Symbols declared in include/sva.h (checked by tests/test_abi.py).
 EXPORTED = [
@@ -252,8 +255,9 @@ class Context:
     def set_path_kernel(self, kernel: int):
         self._chk(lib.sva_set_path_kernel(self.h, kernel))
 
-    def set_timing(self, on: bool):
-        self._chk(lib.sva_set_timing(self.h, 1 if on else 0))
+    def set_timing(self, on):
+        """on: False/True, or SVA_TIMING_PATHS to time only the path kernel."""
+        self._chk(lib.sva_set_timing(self.h, int(on)))
 
     def reset_timing(self):
         self._chk(lib.sva_reset_timing(self.h))

@@ -419,7 +419,7 @@ bool fused_fits(int W, int H, int D, int dmin) {
 hipError_t launch_paths_fused(Ctx& c, const uint64_t* cen, size_t cen_words, size_t map_l,
                               size_t map_r, int W, int H, int D, int dmin, int dir, int P1,
                               int P2, uint8_t* L8) {
-    ScopedKernelTimer t(c, "sgm_paths");
+    DispatchTimer t(c, "sgm_paths");
     if (!paths_supported(D) || !fused_fits(W, H, D, dmin) || cen_words * 8 >= (1ull << 31))
         return hipErrorInvalidValue;
     FusedGeom g;
@@ -445,11 +445,12 @@ hipError_t launch_paths_fused(Ctx& c, const uint64_t* cen, size_t cen_words, siz
 #define SVA_FUSED_LAUNCH(DPL)                                                                   \
     do {                                                                                        \
         if (dir > 0)                                                                            \
-            hipLaunchKernelGGL((sgm_fused_kernel<DPL, 1>), grid, dim3(FBLOCK), 0, c.stream, cen,  \
-                               L8, g);                                                          \
+            hipExtLaunchKernelGGL((sgm_fused_kernel<DPL, 1>), grid, dim3(FBLOCK), 0, c.stream,  \
+                                  t.start, t.stop, 0, cen, L8, g);                              \
         else                                                                                    \
-            hipLaunchKernelGGL((sgm_fused_kernel<DPL, -1>), grid, dim3(FBLOCK), 0, c.stream,    \
-                               cen, L8, g);                                                     \
+            hipExtLaunchKernelGGL((sgm_fused_kernel<DPL, -1>), grid, dim3(FBLOCK), 0, c.stream, \
+                                  t.start, t.stop, 0, cen, L8, g);                              \
+        t.used = true;                                                                          \
     } while (0)
     switch (D) {
         case 64: SVA_FUSED_LAUNCH(4); break;

@@ -72,7 +72,7 @@ bool paths_supported(int D) { return D == 64 || D == 128 || D == 192 || D == 256
 
 hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
                         uint8_t* L8) {
-    ScopedKernelTimer t(c, "sgm_paths");
+    DispatchTimer t(c, "sgm_paths");
     PathGeom g;
     g.W = W; g.H = H; g.D = D; g.P1 = P1; g.P2 = P2;
     g.blk_h = (H + LINES_PER_BLOCK - 1) / LINES_PER_BLOCK;
@@ -117,13 +117,18 @@ hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, i
         return hipGetLastError();
     }
 #endif
+#define SVA_PATHS_LAUNCH(DPL_)                                                               \
+    hipExtLaunchKernelGGL(sgm_paths_kernel<DPL_>, grid, dim3(PATH_BLOCK), 0, c.stream, t.start, \
+                          t.stop, 0, C, L8, g);                                        \
+    t.used = true
     switch (D) {
-        case 64: hipLaunchKernelGGL(sgm_paths_kernel<4>, grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
-        case 128: hipLaunchKernelGGL(sgm_paths_kernel<8>, grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
-        case 192: hipLaunchKernelGGL(sgm_paths_kernel<12>, grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
-        case 256: hipLaunchKernelGGL(sgm_paths_kernel<16>, grid, dim3(PATH_BLOCK), 0, c.stream, C, L8, g); break;
+        case 64: SVA_PATHS_LAUNCH(4); break;
+        case 128: SVA_PATHS_LAUNCH(8); break;
+        case 192: SVA_PATHS_LAUNCH(12); break;
+        case 256: SVA_PATHS_LAUNCH(16); break;
         default: return hipErrorInvalidValue;
     }
+#undef SVA_PATHS_LAUNCH
     return hipGetLastError();
 }
 

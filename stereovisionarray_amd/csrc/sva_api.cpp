@@ -443,7 +443,10 @@ int sva_set_path_kernel(void* ctx, int kernel) {
 int sva_set_timing(void* ctx, int enable) {
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
+    if (enable < 0 || enable > SVA_TIMING_PATHS)
+        return fail(c, SVA_ERR_INVALID_ARG, "timing mode must be 0, 1 or 2");
     c->timer.enabled = enable != 0;
+    c->timer.paths_only = enable == SVA_TIMING_PATHS;
     return SVA_OK;
 }
 

@@ -2,9 +2,11 @@
 // by the C-ABI (sva_api.cpp) and the HIP kernel translation units.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
 #include <map>
 #include <string>
 #include <vector>
@@ -23,6 +25,7 @@ struct Status {
 // while timing is enabled; resolution happens lazily in kernel_time().
 struct KernelTimer {
     bool enabled = false;
+    bool paths_only = false;   // sva_set_timing(ctx, SVA_TIMING_PATHS): "sgm_paths" only
     struct Pending {
         std::string name;
         hipEvent_t start, stop;
@@ -68,10 +71,37 @@ struct ScopedKernelTimer {
     const char* name;
     hipEvent_t start = nullptr;
     ScopedKernelTimer(Ctx& ctx, const char* n) : c(ctx), name(n) {
-        if (c.timer.enabled) c.timer.begin(c.stream, name, &start);
+        if (c.timer.enabled && (!c.timer.paths_only || std::strcmp(name, "sgm_paths") == 0))
+            c.timer.begin(c.stream, name, &start);
     }
     ~ScopedKernelTimer() {
         if (c.timer.enabled && start) c.timer.end(c.stream, name, start);
+    }
+};
+
+// Timing of one launch through hipExtLaunchKernelGGL's start/stop events: the
+// runtime stamps them from the kernel's own dispatch, so no separate event
+// packets enter the stream (used for the path kernel, the one bench.py times
+// inside its timed region).  start/stop stay null when timing is off.
+struct DispatchTimer {
+    Ctx& c;
+    const char* name;
+    hipEvent_t start = nullptr, stop = nullptr;
+    bool used = false;   // set by the launch that received start/stop
+    DispatchTimer(Ctx& ctx, const char* n) : c(ctx), name(n) {
+        if (c.timer.enabled && (!c.timer.paths_only || std::strcmp(name, "sgm_paths") == 0)) {
+            start = c.timer.get_event();
+            stop = start ? c.timer.get_event() : nullptr;
+            if (!stop && start) { c.timer.pool.push_back(start); start = nullptr; }
+        }
+    }
+    ~DispatchTimer() {
+        if (start && stop && used)
+            c.timer.pending.push_back(KernelTimer::Pending{name, start, stop});
+        else if (start && stop) {
+            c.timer.pool.push_back(start);
+            c.timer.pool.push_back(stop);
+        }
     }
 };
 

@@ -138,6 +138,17 @@ def test_reserve_timing_and_errors(ctx, sva):
     with pytest.raises(sva.SvaError) as e:
         ctx.set_path_kernel(7)
     assert e.value.status == sva.SVA_ERR_INVALID_ARG
+    # SVA_TIMING_PATHS: only the path kernel records events (bench.py's timed region)
+    ctx.reset_timing()
+    ctx.set_timing(sva.SVA_TIMING_PATHS)
+    ctx.disparity_sgm(L, R, sva.default_params(D=128))
+    ctx.set_timing(sva.SVA_TIMING_OFF)
+    assert ctx.kernel_time("sgm_paths")[1] == 1
+    for name in ("census", "cost", "wta"):
+        assert ctx.kernel_time(name) == (0.0, 0), name
+    with pytest.raises(sva.SvaError) as e:
+        ctx.set_timing(3)
+    assert e.value.status == sva.SVA_ERR_INVALID_ARG
     assert ctx.kernel_time("no_such_kernel") == (0.0, 0)
     ctx.reset_timing()
     assert ctx.kernel_time("sgm_paths") == (0.0, 0)
