@@ -63,6 +63,11 @@ struct Ctx {
     DevBuf in_c, shifted, keys, counts, total;
     int cu_count = 256;
     int path_kernel = SVA_PATH_KERNEL_AUTO;   // sva_set_path_kernel
+#ifdef SVA_SPLIT_CENSUS   // A/B builds only: separate census + cost launches
+    bool split_census = true;
+#else
+    bool split_census = false;
+#endif
 };
 
 // RAII helper: records timing events around one launch when enabled.
@@ -118,6 +123,10 @@ hipError_t launch_census_pair_padded(Ctx& c, const uint8_t* left, const uint8_t*
                                      int H, size_t pitch, int pr, uint64_t* out_l,
                                      uint64_t* out_r);
 // cost.hip
+// Census + cost in one kernel (census_cost.hip), 1-D steps (dir = +-1).
+bool census_cost_supported(int D);
+hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right, int W, int H,
+                              size_t pitch, int D, int dmin, int dir, uint8_t* C);
 hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,
                        int dmin, int dir, uint8_t* C);
 // sgm_paths.hip -- all 8 directions in one launch; L8 = [8][H][W][D] u8.

@@ -106,9 +106,11 @@ def test_reserve_timing_and_errors(ctx, sva):
     ctx.disparity_sgm(L, R, sva.default_params(D=128))
     ctx.disparity_sgm(L, R, sva.default_params(D=128))
     ctx.set_timing(False)
-    for name in ("census", "cost", "sgm_paths", "wta"):
+    for name in ("cost", "sgm_paths", "wta"):
         ms, n = ctx.kernel_time(name)
         assert n == 2 and ms > 0.0, name
+    # 1-D steps without the L/R check, D >= 128: census and cost are one kernel ("cost")
+    assert ctx.kernel_time("census") == (0.0, 0)
     # the census-fused path kernel has no cost volume and no cost kernel
     ctx.reset_timing()
     ctx.set_path_kernel(sva.SVA_PATH_KERNEL_FUSED)

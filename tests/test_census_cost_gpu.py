@@ -1,0 +1,127 @@
+"""The census+cost kernel (census_cost.hip, sva_census_cost_d) vs the CPU
+oracle's census -> cost, bit-exact, and the pipelines that use it.
+
+The kernel serves sva_disparity_sgm* for 1-D steps without the L/R check, so
+these cases cover its tiling edges: widths that are not a multiple of its
+128-pixel tile, heights below the 7-row window and not a multiple of its
+row band, large dmin (every matched column outside the image), both step
+signs, pitched images, and all four D.
+"""
+import numpy as np
+import pytest
+import torch
+
+from stereovisionarray_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a, d):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(d)
+
+
+def cost_gpu(ctx, sva, L, R, D, dmin, dir, torch_dev, pitch=None):
+    H, W = L.shape
+    if pitch is None:
+        pitch = W
+    Lp = np.zeros((H, pitch), np.uint8)
+    Rp = np.zeros((H, pitch), np.uint8)
+    Lp[:, :W], Rp[:, :W] = L, R
+    Lp[:, W:], Rp[:, W:] = 251, 3      # pitch padding must never be read as pixels
+    dL, dR = dev(Lp, torch_dev), dev(Rp, torch_dev)
+    C = torch.full((H, W, D), 0xAA, dtype=torch.uint8, device=torch_dev)
+    p = sva.default_params(D=D, dmin=dmin, dir=dir)
+    ctx.census_cost_d(dL.data_ptr(), dR.data_ptr(), W, H, pitch, p, C.data_ptr())
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    return C.cpu().numpy()
+
+
+@pytest.mark.parametrize("D", [64, 128, 192, 256])
+@pytest.mark.parametrize("dir,dmin", [(-1, 0), (1, 0), (1, 7), (-1, 13)])
+def test_census_cost_vs_oracle(ctx, sva, oracle, torch_dev, D, dir, dmin):
+    W, H = 333, 21
+    L, R, _ = synth.stereo_pair(H, W, D, dmin, dir, seed=D * 3 + dmin)
+    L[::5, ::3] = 128
+    R[::5, ::3] = 128          # equal neighbours: the census '<' stays strict
+    got = cost_gpu(ctx, sva, L, R, D, dmin, dir, torch_dev)
+    want = oracle.cost(oracle.census(L), oracle.census(R), D, dmin, dir)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("W,H", [(9, 7), (1, 1), (8, 3), (127, 9), (128, 16), (129, 17),
+                                 (257, 5), (300, 40)])
+@pytest.mark.parametrize("dir", [-1, 1])
+def test_census_cost_shapes(ctx, sva, oracle, torch_dev, W, H, dir):
+    D = 64
+    L = synth.texture(H, W, W * 7 + H)
+    R = synth.texture(H, W, W * 11 + H + 1)
+    got = cost_gpu(ctx, sva, L, R, D, 0, dir, torch_dev)
+    want = oracle.cost(oracle.census(L), oracle.census(R), D, 0, dir)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("dmin", [200, 400])
+def test_census_cost_far_dmin(ctx, sva, oracle, torch_dev, dmin):
+    # dmin + D past the width: whole right-word ranges outside the image (62)
+    W, H, D = 260, 12, 128
+    L = synth.texture(H, W, 1)
+    R = synth.texture(H, W, 2)
+    for dir in (-1, 1):
+        got = cost_gpu(ctx, sva, L, R, D, dmin, dir, torch_dev)
+        want = oracle.cost(oracle.census(L), oracle.census(R), D, dmin, dir)
+        assert np.array_equal(got, want)
+
+
+def test_census_cost_pitched(ctx, sva, oracle, torch_dev):
+    W, H, D = 250, 30, 128
+    L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=5)
+    got = cost_gpu(ctx, sva, L, R, D, 0, -1, torch_dev, pitch=320)
+    want = oracle.cost(oracle.census(L), oracle.census(R), D, 0, -1)
+    assert np.array_equal(got, want)
+
+
+def test_census_cost_matches_split_kernels(ctx, sva, torch_dev):
+    # the same bytes as the two-kernel route (census x2 -> cost), 1080p D=128
+    W, H, D = 1920, 1080, 128
+    L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=1)
+    dL, dR = dev(L, torch_dev), dev(R, torch_dev)
+    p = sva.default_params(D=D)
+    cl = torch.zeros((H, W), dtype=torch.int64, device=torch_dev)
+    cr = torch.zeros((H, W), dtype=torch.int64, device=torch_dev)
+    C1 = torch.zeros((H, W, D), dtype=torch.uint8, device=torch_dev)
+    C2 = torch.ones((H, W, D), dtype=torch.uint8, device=torch_dev)
+    ctx.census_d(dL.data_ptr(), W, H, W, cl.data_ptr())
+    ctx.census_d(dR.data_ptr(), W, H, W, cr.data_ptr())
+    ctx.cost_d(cl.data_ptr(), cr.data_ptr(), W, H, p, C1.data_ptr())
+    ctx.census_cost_d(dL.data_ptr(), dR.data_ptr(), W, H, W, p, C2.data_ptr())
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C2)
+
+
+def test_census_cost_rejects_2d_steps(ctx, sva, torch_dev):
+    W, H = 64, 16
+    img = torch.zeros((H, W), dtype=torch.uint8, device=torch_dev)
+    C = torch.zeros((H, W, 64), dtype=torch.uint8, device=torch_dev)
+    p = sva.default_params(D=64)
+    p.dir, p.dir_y = 0, 1
+    with pytest.raises(sva.SvaError) as e:
+        ctx.census_cost_d(img.data_ptr(), img.data_ptr(), W, H, W, p, C.data_ptr())
+    assert e.value.status == sva.SVA_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("D,dir,dmin", [(64, 1, 3), (128, -1, 0), (192, -1, 5), (256, 1, 0)])
+def test_pipeline_through_census_cost(ctx, sva, oracle, D, dir, dmin):
+    # sva_disparity_sgm (no L/R check) now runs census_cost -> paths -> wta
+    W, H = 290, 45
+    L, R, _ = synth.stereo_pair(H, W, D, dmin, dir, seed=D + 1)
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_COST_VOLUME)
+    try:
+        p = sva.default_params(D=D, dmin=dmin, dir=dir, subpixel=1)
+        disp, sub = ctx.disparity_sgm(L, R, p)
+    finally:
+        ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
+    odisp, osub = oracle.sgm(L, R, D, dmin, dir, 10, 120, subpixel=True)
+    assert np.array_equal(disp, odisp)
+    assert np.max(np.abs(sub - osub)) <= 1e-5

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--H", type=int, default=1080)
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--iters", type=int, default=30)
-    ap.add_argument("--entry", default="paths", choices=["paths", "sgm", "cost", "fused", "census"])
+    ap.add_argument("--entry", default="paths", choices=["paths", "sgm", "cost", "fused", "census", "census_cost"])
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -80,6 +80,10 @@ def main():
                 st = lib.sva_paths_fused_d(h, ct.c_void_p(dL.data_ptr()), ct.c_void_p(dR.data_ptr()),
                                            W, H, ct.c_size_t(W), ct.byref(p),
                                            ct.c_void_p(L8.data_ptr()))
+            elif a.entry == "census_cost":
+                st = lib.sva_census_cost_d(h, ct.c_void_p(dL.data_ptr()), ct.c_void_p(dR.data_ptr()),
+                                           W, H, ct.c_size_t(W), ct.byref(p),
+                                           ct.c_void_p(C.data_ptr()))
             elif a.entry == "cost":
                 st = lib.sva_cost_d(h, ct.c_void_p(cl.data_ptr()), ct.c_void_p(cr.data_ptr()), W, H,
                                     ct.byref(p), ct.c_void_p(C.data_ptr()))
@@ -92,6 +96,9 @@ def main():
             e1.synchronize()
             if it >= 2:
                 times[n].append(e0.elapsed_time(e1))
+        if a.entry == "census_cost" and it == 0:   # same bytes as census x2 -> cost
+            torch.cuda.synchronize()
+            assert torch.equal(C, C_src), "census_cost differs from census -> cost"
         if a.entry == "cost" and it == 0:
             outs = []
             for n, lib, h in handles:

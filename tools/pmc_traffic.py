@@ -21,6 +21,7 @@ SHORT = {
     "wta_paths_kernel": "wta", "hamming_cost_kernel": "cost", "census9x7_kernel": "census",
     "hamming_cost2_kernel": "cost2", "fuse_depth_kernel": "fuse_depth",
     "hamming_cost_rows_kernel": "cost", "census9x7_rows_kernel": "census",
+    "census_cost_kernel": "cost",
 }
 
 
