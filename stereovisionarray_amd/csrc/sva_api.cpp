@@ -214,9 +214,9 @@ int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int
                    const sva_sgm_params* p, uint16_t* disp, float* sub) {
     if (use_fused(c, p, W, H)) return run_sgm_fused(c, left, right, W, H, pitch, p, disp, sub);
     const size_t np = (size_t)W * H, nv = np * (size_t)p->D;
-    if (p->dir_y == 0 && !p->lr_check && p->D >= 128 && census_cost_supported(p->D) &&
-        !c->split_census) {
-        // census maps stay on chip: one census+cost kernel (census_cost.hip).
+    if (p->dir_y == 0 && p->D >= 128 && census_cost_supported(p->D) && !c->split_census) {
+        // census maps stay on chip: one census+cost kernel (census_cost.hip),
+        // once per matching role when the L/R check runs.
         // In-process A/B per frame at 1080p: D=128 1.129 -> 1.112 ms,
         // D=192 1.646 -> 1.588 ms; D=64 is faster split (0.609 vs 0.650 ms).
         SVA_HIP(c, c->cost.ensure(nv), "cost workspace");
@@ -227,6 +227,18 @@ int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int
                 "cost launch");
         SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
         SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, disp, sub), "wta launch");
+        if (p->lr_check) {
+            // right image as reference: the images swap roles, the step flips
+            SVA_HIP(c, c->disp_r.ensure(np * 2), "lr workspace");
+            uint16_t* dr = (uint16_t*)c->disp_r.ptr;
+            SVA_HIP(c, launch_census_cost(*c, right, left, W, H, pitch, p->D, p->dmin, -p->dir, C),
+                    "cost launch");
+            SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
+            SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, dr, nullptr),
+                    "wta launch");
+            SVA_HIP(c, launch_lr_check(*c, disp, dr, W, H, p->dir, 0, p->lr_max_diff, p->invalid),
+                    "lr launch");
+        }
         return SVA_OK;
     }
     SVA_HIP(c, c->census_l.ensure(np * 8), "census workspace");

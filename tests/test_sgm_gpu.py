@@ -170,14 +170,17 @@ def test_full_pipeline_device_buffers(ctx, sva, oracle, torch_dev):
     assert np.array_equal(host(disp).view(np.uint16), od)
 
 
-def test_lr_check(ctx, sva, oracle):
-    W, H, D = 180, 60, 64
-    L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=11, stripes=6, step=9)
-    p = sva.default_params(D=D, lr_check=1, lr_max_diff=1, invalid=0xFFFF)
+# D = 64 runs census + cost kernels, D >= 128 the census+cost kernel for both
+# matching roles (the right-reference pass swaps the images, not census maps)
+@pytest.mark.parametrize("D,dir,dmin", [(64, -1, 0), (128, -1, 0), (128, 1, 3), (192, -1, 2)])
+def test_lr_check(ctx, sva, oracle, D, dir, dmin):
+    W, H = 300, 60
+    L, R, _ = synth.stereo_pair(H, W, D, dmin, dir, seed=11, stripes=6, step=9)
+    p = sva.default_params(D=D, dmin=dmin, dir=dir, lr_check=1, lr_max_diff=1, invalid=0xFFFF)
     disp, _ = ctx.disparity_sgm(L, R, p)
-    dl, _ = oracle.sgm(L, R, D, 0, -1, subpixel=False, threads=8)
-    dr, _ = oracle.sgm(R, L, D, 0, 1, subpixel=False, threads=8)
-    exp = oracle.lr_check(dl, dr, -1, 1, 0xFFFF)
+    dl, _ = oracle.sgm(L, R, D, dmin, dir, subpixel=False, threads=8)
+    dr, _ = oracle.sgm(R, L, D, dmin, -dir, subpixel=False, threads=8)
+    exp = oracle.lr_check(dl, dr, dir, 1, 0xFFFF)
     assert np.array_equal(disp, exp)
     assert (disp == 0xFFFF).any() and (disp != 0xFFFF).any()
 
