@@ -81,7 +81,7 @@ hipError_t DevBuf::ensure(size_t n) {
         bytes = 0;
     }
     size_t want = std::max<size_t>(n, 256);
-    hipError_t e = hipMalloc(&ptr, want);
+    hipError_t e = flags ? hipExtMallocWithFlags(&ptr, want, flags) : hipMalloc(&ptr, want);
     if (e != hipSuccess) {
         ptr = nullptr;
         return e;
@@ -404,6 +404,9 @@ int sva_create(int device, void** out) {
         return SVA_ERR_DEVICE;
     }
     c->stream = c->own_stream;
+#ifdef SVA_PATHS_MALLOC_FLAGS   // A/B builds only: allocation flags of the path volumes
+    c->paths.flags = SVA_PATHS_MALLOC_FLAGS;
+#endif
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->cu_count = prop.multiProcessorCount;
     *out = c;

@@ -45,6 +45,7 @@ struct KernelTimer {
 struct DevBuf {
     void* ptr = nullptr;
     size_t bytes = 0;
+    unsigned flags = 0;   // hipExtMallocWithFlags flags (0 = hipMalloc)
     hipError_t ensure(size_t n);
     void release();
 };
