@@ -245,6 +245,13 @@ template <int DPL> constexpr int pf_v() {
     return DPL == 4 ? SVA_PF_V4 : DPL == 8 ? SVA_PF_V8 : DPL == 12 ? SVA_PF_V12 : SVA_PF_V16;
 }
 
+#ifdef SVA_PATHS_TRACE
+// Experiment builds only: per-wave s_memrealtime stamps every 96 steps
+// (tools/paths_trace.py), [wave][0] = direction, [wave][1 + t/96] = stamp.
+__device__ unsigned long long* g_paths_trace;
+constexpr int kTraceSlots = 32;
+#endif
+
 // One path line over a materialised cost volume C.
 template <int DPL, bool DIAG, int VAR, int PF>
 __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& g, int rx, int ry,
@@ -315,7 +322,16 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
     };
 
     int t = 0;
+#ifdef SVA_PATHS_TRACE
+    const unsigned wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+    unsigned long long* tr = g_paths_trace + (size_t)wid * kTraceSlots;
+    const bool rec = (threadIdx.x & 63) == 0;
+    if (rec) tr[0] = (unsigned long long)(10 + (rx + 1) * 3 + (ry + 1));
+#endif
     for (; t + PF <= steps; t += PF) {
+#ifdef SVA_PATHS_TRACE
+        if (rec && t % 96 == 0 && 1 + t / 96 < kTraceSlots) tr[1 + t / 96] = __builtin_amdgcn_s_memrealtime();
+#endif
 #pragma unroll
         for (int p = 0; p < PF; p++) step(p, true);
     }

@@ -43,7 +43,11 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
                                                                PathGeom g) {
     // Horizontal directions (W steps per line, the longest) get the lowest
     // block ids and issue priority so they are never the tail.
+#ifndef SVA_PATHS_ORDER
+#define SVA_PATHS_ORDER 0
+#endif
     int b = blockIdx.x, r, lb;
+#if SVA_PATHS_ORDER == 0
     if (b < 2 * g.blk_h) {
         r = b / g.blk_h;
         lb = b - r * g.blk_h;
@@ -53,6 +57,25 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
         r = 2 + b / g.blk_w;
         lb = b - (r - 2) * g.blk_w;
     }
+#else
+    // experiment: diagonals first, then horizontal, up, down (the fastest last)
+    {
+        constexpr int ORD[8] = {4, 5, 6, 7, 0, 1, 3, 2};
+        r = ORD[7];
+        lb = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int nb = ORD[i] < 2 ? g.blk_h : g.blk_w;
+            if (b < nb) { r = ORD[i]; lb = b; break; }
+            b -= nb;
+        }
+#if SVA_PATHS_ORDER == 1
+        if (r < 2) __builtin_amdgcn_s_setprio(1);
+#elif SVA_PATHS_ORDER == 2
+        if (r >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+    }
+#endif
     const int line = lb * LINES_PER_BLOCK + (threadIdx.x >> 4);
     const int k = threadIdx.x & 15;
     const int nlines = r < 2 ? g.H : g.W;
@@ -68,11 +91,35 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
 
 }  // namespace
 
+#ifdef SVA_PATHS_TRACE
+unsigned long long*& trace_buffer() {
+    static unsigned long long* p = nullptr;
+    return p;
+}
+extern "C" int sva_debug_paths_trace_copy(void* host, size_t bytes) {
+    if (!trace_buffer()) return 1;
+    return hipMemcpy(host, trace_buffer(), bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 2;
+}
+#endif
+
 bool paths_supported(int D) { return D == 64 || D == 128 || D == 192 || D == 256; }
 
 hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
                         uint8_t* L8) {
     DispatchTimer t(c, "sgm_paths");
+#ifdef SVA_PATHS_TRACE
+    {
+        static unsigned long long* buf = nullptr;
+        const size_t n = (size_t)4 * 65536 * kTraceSlots;
+        if (!buf) {
+            if (hipMalloc(&buf, n * 8) != hipSuccess) return hipErrorOutOfMemory;
+            if (hipMemcpyToSymbol(HIP_SYMBOL(g_paths_trace), &buf, sizeof(buf)) != hipSuccess)
+                return hipErrorInvalidValue;
+        }
+        (void)hipMemsetAsync(buf, 0, n * 8, c.stream);
+        trace_buffer() = buf;
+    }
+#endif
     PathGeom g;
     g.W = W; g.H = H; g.D = D; g.P1 = P1; g.P2 = P2;
     g.blk_h = (H + LINES_PER_BLOCK - 1) / LINES_PER_BLOCK;
