@@ -165,11 +165,10 @@ __global__ __launch_bounds__(CC_BLOCK) void census_cost_kernel(
             const int y = y0 + p - 1;
             const uint64_t* rwb = rw[(p - 1) & 1];
             const uint64_t* lwb = lw[(p - 1) & 1];
-            // a wave owns 16 pixels x all NC chunks per pass, so its stores fill
-            // whole 128-byte lines (a half-line split across waves made the
-            // TCC write 1.27x the volume); lane (p, c) forms chunks c, c+4, ...
-            // and each 32-lane LDS group reads 16 pixels x 2 chunks: 32
-            // consecutive words, conflict-free
+            // a wave owns 16 pixels x all NC chunks per pass (lane (p, c) forms
+            // chunks c, c+4, ...), so each 128-byte line is written by one wave
+            // in back-to-back instructions; each 32-lane LDS group reads 16
+            // pixels x 2 chunks: 32 consecutive words, conflict-free
             const int wv = t >> 6, ln = t & 63;
             const int pl = ln & 15, c0 = ln >> 4;
 #pragma unroll

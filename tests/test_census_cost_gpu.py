@@ -61,6 +61,18 @@ def test_census_cost_shapes(ctx, sva, oracle, torch_dev, W, H, dir):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("D", [128, 192, 256])
+@pytest.mark.parametrize("W,H", [(1, 1), (9, 8), (129, 5), (300, 13)])
+def test_census_cost_shapes_wide_d(ctx, sva, oracle, torch_dev, D, W, H):
+    # right-word ranges of 128 + D - 1 columns over images narrower than one tile
+    for dir in (-1, 1):
+        L = synth.texture(H, W, W * 5 + D)
+        R = synth.texture(H, W, W * 3 + D + 1)
+        got = cost_gpu(ctx, sva, L, R, D, 1, dir, torch_dev)
+        want = oracle.cost(oracle.census(L), oracle.census(R), D, 1, dir)
+        assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("dmin", [200, 400])
 def test_census_cost_far_dmin(ctx, sva, oracle, torch_dev, dmin):
     # dmin + D past the width: whole right-word ranges outside the image (62)
