@@ -382,10 +382,31 @@ def run_array(a, wl, world, rank, local, dev):
     depth = torch.zeros((len(groups), H, W), dtype=torch.float64, device=dev)
     nvalid = torch.zeros((len(groups), H, W), dtype=torch.uint8, device=dev)
     maps = {"all": None}
+    # pairs alternate over n_streams contexts (own stream and workspaces) so
+    # consecutive pairs overlap; gather and fusion wait for all of them
+    n_streams = a.streams if a.streams > 0 else (2 if len(jobs) > 1 else 1)
+    ctxs, cstreams = [ctx], [stream]
+    for _ in range(1, n_streams):
+        s_ = torch.cuda.Stream(dev)
+        c_ = sva.Context(local)
+        c_.set_stream(s_.cuda_stream)
+        c_.reserve(W, H, D)
+        ctxs.append(c_)
+        cstreams.append(s_)
 
     def step():
+        if len(ctxs) > 1:                # the previous step's fusion has read disp
+            go = torch.cuda.Event()
+            go.record(stream)
+            for s_ in cstreams[1:]:
+                s_.wait_event(go)
         for jb, (L, R, p) in enumerate(jobs):
-            ctx.disparity_sgm_d(L.data_ptr(), R.data_ptr(), W, H, W, p, disp[jb].data_ptr())
+            ctxs[jb % len(ctxs)].disparity_sgm_d(L.data_ptr(), R.data_ptr(), W, H, W, p,
+                                                 disp[jb].data_ptr())
+        for s_ in cstreams[1:]:
+            done_ = torch.cuda.Event()
+            done_.record(s_)
+            stream.wait_event(done_)
         if world > 1:
             if a.dist_backend == "nccl":
                 allm = sdist.gather_maps(disp, n_units, dst=0)
@@ -400,8 +421,8 @@ def run_array(a, wl, world, rank, local, dev):
                                  depth[g].data_ptr(), nvalid[g].data_ptr())
             maps["all"] = allm
 
-    elapsed = timed(a, step, world, dev, ctx)
-    kernels = breakdown(a, step, world, ctx, kernel_table(ctx))
+    elapsed = timed(a, step, world, dev, ctxs)
+    kernels = breakdown(a, step, world, ctxs, kernel_table(ctxs))
     value = n_units * W * H * D * a.steps / elapsed / 1e6
     out = None
     if rank == 0:
@@ -436,7 +457,8 @@ def run_array(a, wl, world, rank, local, dev):
                                    "Mode S along each pair's baseline step, RCCL gather, "
                                    "per-camera median fusion on rank 0",
                        "W": W, "H": H, "D": D, "P1": 10, "P2": 120, "pairs": n_units,
-                       "parallelism": f"pairs sharded over {world} rank(s), gather to rank 0"},
+                       "parallelism": f"pairs sharded over {world} rank(s), gather to rank 0",
+                       "streams_per_rank": len(ctxs)},
             "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
             "fused_maps_per_s": round(len(groups) * a.steps / elapsed, 2),
             "ref_interior_depth_exact_frac": round(exact, 4),
@@ -446,7 +468,8 @@ def run_array(a, wl, world, rank, local, dev):
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(W, H, D, a.cpu_threads)
         print(json.dumps(out), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
 
