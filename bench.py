@@ -223,8 +223,8 @@ def frame_overlap_beside(W, H, D, frames=40, rounds=2):
     return res
 
 
-def load_traffic(workload):
-    """HBM bytes per sgm_paths launch from the committed rocprofv3 PMC pass
+def load_traffic(workload, kernel="sgm_paths"):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass
     (profiles/pmc_<workload>.json, written by tools/pmc_traffic.py), or None."""
     p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(p):
@@ -232,7 +232,7 @@ def load_traffic(workload):
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get("kernels", {}).get("sgm_paths", {}).get("hbm_bytes_per_launch")
+        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
 
@@ -290,12 +290,13 @@ def breakdown(a, step, world, ctx, timed_kernels):
     kernels = kernel_table(ctxs)
     for c in ctxs:
         c.set_timing(0)
-    if "sgm_paths" in timed_kernels:
-        kernels["sgm_paths"] = timed_kernels["sgm_paths"]
+    for name in ("sgm_paths", "sgm_fused"):
+        if name in timed_kernels:
+            kernels[name] = timed_kernels[name]
     return kernels
 
 
-def kernel_table(ctx, names=("census", "cost", "sgm_paths", "wta", "fuse_depth")):
+def kernel_table(ctx, names=("census", "cost", "sgm_paths", "sgm_fused", "wta", "fuse_depth")):
     """Average hipEvent duration per kernel, pooled over one or several contexts
     (with --streams > 1 the launches overlap, so durations include contention)."""
     ctxs = ctx if isinstance(ctx, list) else [ctx]
@@ -310,17 +311,35 @@ def kernel_table(ctx, names=("census", "cost", "sgm_paths", "wta", "fuse_depth")
     return kernels
 
 
-def roofline_of(kernels, W, H, D, workload):
-    agg = kernels.get("sgm_paths")
+# Algorithmic bytes per launch of each path-aggregation kernel:
+#   sgm_paths: SURVEY.md §8(d)'s aggregation model, 10 B/disp (8 u8 C reads + one
+#              u16 S write), whatever the kernel spills;
+#   sgm_fused: forms C in registers, so its own model is the 8 u8 L_r volumes it
+#              writes (8 B/disp) + the two census maps read once (16 B/px).
+PATH_MODELS = {
+    "sgm_paths": (AGG_BYTES_PER_DISP, 0.0, "SURVEY §8d aggregation: 10 B/disp"),
+    "sgm_fused": (8.0, 16.0, "fused: 8 B/disp L_r writes + 16 B/px census reads"),
+}
+
+
+def roofline_of(kernels, W, H, D, workload, overlapped=False):
+    name = "sgm_paths" if "sgm_paths" in kernels else "sgm_fused"
+    agg = kernels.get(name)
     if not agg:
         return None
-    alg_bytes = AGG_BYTES_PER_DISP * W * H * D
+    per_disp, per_px, model = PATH_MODELS[name]
+    alg_bytes = per_disp * W * H * D + per_px * W * H
     achieved = alg_bytes / (agg["avg_ms"] * 1e-3) / 1e9
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": load_traffic(workload),
-            "kernel": "sgm_paths", "kernel_avg_ms": round(agg["avg_ms"], 4),
-            "alg_bytes_per_launch": alg_bytes}
+    out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+           "traffic": load_traffic(workload, name),
+           "kernel": name, "kernel_avg_ms": round(agg["avg_ms"], 4),
+           "alg_bytes_per_launch": alg_bytes, "model": model}
+    if overlapped:
+        # pairs overlap on several streams: a launch's event span includes the
+        # other stream's kernels, so this fraction is not the single-stream one
+        out["overlapped"] = True
+    return out
 
 
 def rig_of(name):
@@ -462,7 +481,7 @@ def run_array(a, wl, world, rank, local, dev):
             "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
             "fused_maps_per_s": round(len(groups) * a.steps / elapsed, 2),
             "ref_interior_depth_exact_frac": round(exact, 4),
-            "roofline": roofline_of(kernels, W, H, D, "1080p_d128"),
+            "roofline": roofline_of(kernels, W, H, D, "1080p_d128", overlapped=len(ctxs) > 1),
             "cpu_baseline": None,
         }
         if world == 1 and not a.no_cpu_baseline:
@@ -614,7 +633,7 @@ def main():
     disparities = units * W * H * D
     value = disparities / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1e3
-    roofline = roofline_of(kernels, W, H, D, a.workload)
+    roofline = roofline_of(kernels, W, H, D, a.workload, overlapped=len(ctxs) > 1)
     out = {
         "metric": "Mdisparities/sec (W·H·D/s) at 1080p D=128" if a.workload == "1080p_d128"
                   else f"Mdisparities/sec (W·H·D/s) {a.workload}",

@@ -113,7 +113,7 @@ int sva_set_path_kernel(void* ctx, int kernel);
 
 /* Kernel timing with hipEvents on the context stream (measurement only).
  * enable: SVA_TIMING_OFF, SVA_TIMING_ALL (every launch), or SVA_TIMING_PATHS
- * (only the path-aggregation launch "sgm_paths": two event records per frame
+ * (only the path-aggregation launch, "sgm_paths" or "sgm_fused": two event records per frame
  * instead of eight; each record costs a few microseconds of stream time). */
 #define SVA_TIMING_OFF 0
 #define SVA_TIMING_ALL 1

@@ -59,6 +59,7 @@ def _load():
         "svo_wta": (None, [vp, i32, i32, i32, i32, vp, vp]),
         "svo_sgm": (None, [vp, vp, i32, i32, ct.c_ssize_t, i32, i32, i32, i32, i32, vp, vp, i32]),
         "svo_lr_check": (None, [vp, vp, i32, i32, i32, i32, ct.c_uint16]),
+        "svo_lr_sub": (None, [vp, vp, ct.c_size_t, ct.c_uint16]),
         "svo_step_offset": (None, [i32, i32, i32, P(i32), P(i32)]),
         "svo_shift_perspective": (None, [P(OCamera), P(OCamera), vp, vp, i32, i32,
                                          ct.c_ssize_t, vp]),
@@ -206,6 +207,15 @@ def lr_check(disp_l, disp_r, dir, max_diff=1, invalid=0xFFFF):
     H, W = dl.shape
     lib.svo_lr_check(_p(dl), _p(dr), W, H, dir, max_diff, invalid)
     return dl
+
+
+def lr_sub(disp, sub, invalid=0xFFFF):
+    """the f32 map is NaN wherever the checked disparity is
+    `invalid`."""
+    d = _c(disp, np.uint16)
+    out = _c(sub, np.float32).copy()
+    lib.svo_lr_sub(_p(d), _p(out), d.size, invalid)
+    return out
 
 
 def step_offset(s, bx, by):

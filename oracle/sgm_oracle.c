@@ -18,6 +18,7 @@
  * arithmetic is the same either way. */
 static int g_threads = 1;
 
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -289,6 +290,14 @@ void svo_lr_check2(uint16_t* disp_l, const uint16_t* disp_r, int W, int H, int s
             if (diff < 0) diff = -diff;
             if (dr == invalid || diff > max_diff) *dl = invalid;
         }
+}
+
+/* DESIGN.md §2.5 -- the sub-pixel map follows the check: NaN wherever the
+ * disparity is `invalid` after it (a caller building depth from
+ * the f32 map must not see a parabola value for a rejected pixel). */
+void svo_lr_sub(const uint16_t* disp, float* sub, size_t n, uint16_t invalid) {
+    for (size_t i = 0; i < n; i++)
+        if (disp[i] == invalid) sub[i] = NAN;
 }
 
 /* DESIGN.md §2.6 -- median depth over the valid maps (insertion sort). */

@@ -419,7 +419,7 @@ bool fused_fits(int W, int H, int D, int dmin) {
 hipError_t launch_paths_fused(Ctx& c, const uint64_t* cen, size_t cen_words, size_t map_l,
                               size_t map_r, int W, int H, int D, int dmin, int dir, int P1,
                               int P2, uint8_t* L8) {
-    DispatchTimer t(c, "sgm_paths");
+    DispatchTimer t(c, "sgm_fused");
     if (!paths_supported(D) || !fused_fits(W, H, D, dmin) || cen_words * 8 >= (1ull << 31))
         return hipErrorInvalidValue;
     FusedGeom g;

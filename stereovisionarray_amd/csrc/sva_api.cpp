@@ -135,7 +135,10 @@ int check_image(Ctx* c, const void* a, int W, int H, size_t pitch) {
     return SVA_OK;
 }
 
-int check_sgm(Ctx* c, const sva_sgm_params* p, int W) {
+// Shape limits are checked here, before any workspace is allocated: kernels
+// launch with gridDim.y = H (lr_check, refine's gathers), which caps H at
+// 65535, and every path volume is addressed with 32-bit buffer offsets.
+int check_sgm(Ctx* c, const sva_sgm_params* p, int W, int H) {
     if (!p) return fail(c, SVA_ERR_INVALID_ARG, "null params");
     if (p->D <= 0) return fail(c, SVA_ERR_INVALID_ARG, "D must be positive");
     if (!paths_supported(p->D))
@@ -150,7 +153,10 @@ int check_sgm(Ctx* c, const sva_sgm_params* p, int W) {
         return fail(c, SVA_ERR_INVALID_ARG, "penalties must satisfy 0 <= P1, P2 <= 193");
     if (p->lr_check && p->lr_max_diff < 0)
         return fail(c, SVA_ERR_INVALID_ARG, "lr_max_diff must be >= 0");
-    (void)W;
+    if (H > 65535) return fail(c, SVA_ERR_UNSUPPORTED, "H must be <= 65535");
+    if (W > 0 && H > 0 && (unsigned long long)W * (unsigned long long)H * (unsigned)p->D >=
+                              (1ull << 32))
+        return fail(c, SVA_ERR_UNSUPPORTED, "W*H*D must be < 2^32 (32-bit volume offsets)");
     return SVA_OK;
 }
 
@@ -203,7 +209,7 @@ int run_sgm_fused(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int 
         // right image as reference: the census maps swap roles, the step flips
         if ((s = fused_paths(c, mw, true, W, H, p, -dir, L8))) return s;
         SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, dr, nullptr), "wta launch");
-        SVA_HIP(c, launch_lr_check(*c, disp, dr, W, H, dir, 0, p->lr_max_diff, p->invalid),
+        SVA_HIP(c, launch_lr_check(*c, disp, dr, sub, W, H, dir, 0, p->lr_max_diff, p->invalid),
                 "lr launch");
     }
     return SVA_OK;
@@ -236,7 +242,7 @@ int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int
             SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
             SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, dr, nullptr),
                     "wta launch");
-            SVA_HIP(c, launch_lr_check(*c, disp, dr, W, H, p->dir, 0, p->lr_max_diff, p->invalid),
+            SVA_HIP(c, launch_lr_check(*c, disp, dr, sub, W, H, p->dir, 0, p->lr_max_diff, p->invalid),
                     "lr launch");
         }
         return SVA_OK;
@@ -261,7 +267,7 @@ int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int
                 "cost launch");
         SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
         SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, dr, nullptr), "wta launch");
-        SVA_HIP(c, launch_lr_check(*c, disp, dr, W, H, p->dir, p->dir_y, p->lr_max_diff,
+        SVA_HIP(c, launch_lr_check(*c, disp, dr, sub, W, H, p->dir, p->dir_y, p->lr_max_diff,
                                    p->invalid),
                 "lr launch");
     }
@@ -304,6 +310,7 @@ int check_planes(Ctx* c, int W, int H, size_t pitch) {
     if (W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "image size must be positive");
     if (pitch < (size_t)W) return fail(c, SVA_ERR_INVALID_ARG, "pitch smaller than width");
     if ((long long)W * H > (1ll << 31) - 1) return fail(c, SVA_ERR_INVALID_ARG, "image too large");
+    if (H > 65535) return fail(c, SVA_ERR_UNSUPPORTED, "H must be <= 65535 (gridDim.y)");
     return SVA_OK;
 }
 
@@ -508,7 +515,7 @@ int sva_disparity_sgm_d(void* ctx, const uint8_t* left, const uint8_t* right, in
     SVA_CHECK_CTX(c);
     int s;
     if ((s = check_image(c, left, W, H, pitch)) || (s = check_image(c, right, W, H, pitch)) ||
-        (s = check_sgm(c, p, W)))
+        (s = check_sgm(c, p, W, H)))
         return s;
     if (!disp) return fail(c, SVA_ERR_INVALID_ARG, "null disparity output");
     return run_sgm_device(c, left, right, W, H, pitch, p, disp, p->subpixel ? sub : nullptr);
@@ -520,7 +527,7 @@ int sva_disparity_sgm(void* ctx, const uint8_t* left, const uint8_t* right, int 
     SVA_CHECK_CTX(c);
     int s;
     if ((s = check_image(c, left, W, H, pitch)) || (s = check_image(c, right, W, H, pitch)) ||
-        (s = check_sgm(c, p, W)))
+        (s = check_sgm(c, p, W, H)))
         return s;
     if (!disp) return fail(c, SVA_ERR_INVALID_ARG, "null disparity output");
     const bool want_sub = p->subpixel && sub;
@@ -560,7 +567,7 @@ int sva_cost_d(void* ctx, const uint64_t* cl, const uint64_t* cr, int W, int H,
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
-    if ((s = check_sgm(c, p, W))) return s;
+    if ((s = check_sgm(c, p, W, H))) return s;
     if (!cl || !cr || !C || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
     SVA_HIP(c, launch_cost2(*c, cl, cr, W, H, p->D, p->dmin, p->dir, p->dir_y, C), "cost launch");
     return SVA_OK;
@@ -571,7 +578,7 @@ int sva_census_cost_d(void* ctx, const uint8_t* left, const uint8_t* right, int 
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
-    if ((s = check_sgm(c, p, W))) return s;
+    if ((s = check_sgm(c, p, W, H))) return s;
     if ((s = check_image(c, left, W, H, pitch))) return s;
     if ((s = check_image(c, right, W, H, pitch))) return s;
     if (!C) return fail(c, SVA_ERR_INVALID_ARG, "null cost output");
@@ -586,7 +593,7 @@ int sva_paths_d(void* ctx, const uint8_t* C, int W, int H, const sva_sgm_params*
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
-    if ((s = check_sgm(c, p, W))) return s;
+    if ((s = check_sgm(c, p, W, H))) return s;
     if (!C || !L8 || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
     SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
     return SVA_OK;
@@ -598,7 +605,7 @@ int sva_paths_fused_d(void* ctx, const uint8_t* left, const uint8_t* right, int 
     SVA_CHECK_CTX(c);
     int s;
     if ((s = check_image(c, left, W, H, pitch)) || (s = check_image(c, right, W, H, pitch)) ||
-        (s = check_sgm(c, p, W)))
+        (s = check_sgm(c, p, W, H)))
         return s;
     if (!L8) return fail(c, SVA_ERR_INVALID_ARG, "null path volume output");
     if (p->dir_y != 0 || !fused_fits(W, H, p->D, p->dmin))
@@ -614,7 +621,7 @@ int sva_aggregate_d(void* ctx, const uint8_t* C, int W, int H, const sva_sgm_par
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
-    if ((s = check_sgm(c, p, W))) return s;
+    if ((s = check_sgm(c, p, W, H))) return s;
     if (!C || !S || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
     const size_t nv = (size_t)W * H * (size_t)p->D;
     SVA_HIP(c, c->paths.ensure(nv * 8), "path workspace");
@@ -629,7 +636,7 @@ int sva_wta_d(void* ctx, const uint16_t* S, int W, int H, const sva_sgm_params* 
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
-    if ((s = check_sgm(c, p, W))) return s;
+    if ((s = check_sgm(c, p, W, H))) return s;
     if (!S || !disp || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
     SVA_HIP(c, launch_wta_from_sum(*c, S, W, H, p->D, p->dmin, disp, p->subpixel ? sub : nullptr),
             "wta launch");

@@ -25,7 +25,7 @@ struct Status {
 // while timing is enabled; resolution happens lazily in kernel_time().
 struct KernelTimer {
     bool enabled = false;
-    bool paths_only = false;   // sva_set_timing(ctx, SVA_TIMING_PATHS): "sgm_paths" only
+    bool paths_only = false;   // sva_set_timing(ctx, SVA_TIMING_PATHS): path kernels only
     struct Pending {
         std::string name;
         hipEvent_t start, stop;
@@ -71,13 +71,20 @@ struct Ctx {
 #endif
 };
 
+// The path-aggregation launches, the only ones SVA_TIMING_PATHS times:
+// "sgm_paths" reads the cost volume, "sgm_fused" forms the costs itself
+// (each has its own byte model in bench.py).
+inline bool is_path_kernel(const char* name) {
+    return std::strcmp(name, "sgm_paths") == 0 || std::strcmp(name, "sgm_fused") == 0;
+}
+
 // RAII helper: records timing events around one launch when enabled.
 struct ScopedKernelTimer {
     Ctx& c;
     const char* name;
     hipEvent_t start = nullptr;
     ScopedKernelTimer(Ctx& ctx, const char* n) : c(ctx), name(n) {
-        if (c.timer.enabled && (!c.timer.paths_only || std::strcmp(name, "sgm_paths") == 0))
+        if (c.timer.enabled && (!c.timer.paths_only || is_path_kernel(name)))
             c.timer.begin(c.stream, name, &start);
     }
     ~ScopedKernelTimer() {
@@ -95,7 +102,7 @@ struct DispatchTimer {
     hipEvent_t start = nullptr, stop = nullptr;
     bool used = false;   // set by the launch that received start/stop
     DispatchTimer(Ctx& ctx, const char* n) : c(ctx), name(n) {
-        if (c.timer.enabled && (!c.timer.paths_only || std::strcmp(name, "sgm_paths") == 0)) {
+        if (c.timer.enabled && (!c.timer.paths_only || is_path_kernel(name))) {
             start = c.timer.get_event();
             stop = start ? c.timer.get_event() : nullptr;
             if (!stop && start) { c.timer.pool.push_back(start); start = nullptr; }
@@ -148,7 +155,7 @@ hipError_t launch_wta_from_paths(Ctx& c, const uint8_t* L8, int W, int H, int D,
                                  uint16_t* disp, float* sub);
 hipError_t launch_wta_from_sum(Ctx& c, const uint16_t* S, int W, int H, int D, int dmin,
                                uint16_t* disp, float* sub);
-hipError_t launch_lr_check(Ctx& c, uint16_t* disp_l, const uint16_t* disp_r, int W, int H,
+hipError_t launch_lr_check(Ctx& c, uint16_t* disp_l, const uint16_t* disp_r, float* sub, int W, int H,
                            int sx, int sy, int max_diff, uint16_t invalid);
 // 2-D matching step (sy != 0); sy == 0 forwards to launch_cost(dir = sx).
 hipError_t launch_cost2(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,

@@ -177,19 +177,29 @@ __global__ __launch_bounds__(BLOCK) void wta_sum_kernel(const uint16_t* __restri
     wta_finish<DPL>(S, k, D, dmin, pix, disp, sub);
 }
 
-__global__ void lr_check_kernel(uint16_t* __restrict__ dl, const uint16_t* __restrict__ dr, int W,
-                                int H, int sx, int sy, int max_diff, uint16_t invalid) {
+// DESIGN.md §2.5.  The sub-pixel map (nullable) follows the check: NaN
+// wherever the disparity is `invalid` afterwards (oracle svo_lr_sub).
+__global__ void lr_check_kernel(uint16_t* __restrict__ dl, const uint16_t* __restrict__ dr,
+                                float* __restrict__ sub, int W, int H, int sx, int sy,
+                                int max_diff, uint16_t invalid) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     if (x >= W) return;
-    uint16_t* p = dl + (size_t)y * W + x;
-    const int d = *p;
-    if (d == invalid) return;
-    const int2 o = step_offset(d, sx, sy);
-    const int xr = x + o.x, yr = y + o.y;
-    if (xr < 0 || xr >= W || yr < 0 || yr >= H) { *p = invalid; return; }
-    const int r = dr[(size_t)yr * W + xr];
-    const int diff = d > r ? d - r : r - d;
-    if (r == invalid || diff > max_diff) *p = invalid;
+    const size_t i = (size_t)y * W + x;
+    const int d = dl[i];
+    bool bad = d == invalid;
+    if (!bad) {
+        const int2 o = step_offset(d, sx, sy);
+        const int xr = x + o.x, yr = y + o.y;
+        if (xr < 0 || xr >= W || yr < 0 || yr >= H) {
+            bad = true;
+        } else {
+            const int r = dr[(size_t)yr * W + xr];
+            const int diff = d > r ? d - r : r - d;
+            bad = r == invalid || diff > max_diff;
+        }
+        if (bad) dl[i] = invalid;
+    }
+    if (bad && sub) sub[i] = __builtin_nanf("");
 }
 
 }  // namespace
@@ -239,12 +249,12 @@ hipError_t launch_wta_from_sum(Ctx& c, const uint16_t* S, int W, int H, int D, i
     return hipGetLastError();
 }
 
-hipError_t launch_lr_check(Ctx& c, uint16_t* disp_l, const uint16_t* disp_r, int W, int H,
-                           int sx, int sy, int max_diff, uint16_t invalid) {
+hipError_t launch_lr_check(Ctx& c, uint16_t* disp_l, const uint16_t* disp_r, float* sub, int W,
+                           int H, int sx, int sy, int max_diff, uint16_t invalid) {
     ScopedKernelTimer t(c, "lr_check");
     dim3 grid((W + 255) / 256, H);
-    hipLaunchKernelGGL(lr_check_kernel, grid, dim3(256), 0, c.stream, disp_l, disp_r, W, H, sx, sy,
-                       max_diff, invalid);
+    hipLaunchKernelGGL(lr_check_kernel, grid, dim3(256), 0, c.stream, disp_l, disp_r, sub, W, H,
+                       sx, sy, max_diff, invalid);
     return hipGetLastError();
 }
 

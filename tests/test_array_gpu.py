@@ -13,6 +13,8 @@ import torch
 
 from stereovisionarray_amd import synth
 
+from checks import assert_sub_close
+
 pytestmark = pytest.mark.gpu
 
 SUB_TOL = 1e-5
@@ -96,13 +98,14 @@ def test_vertical_shift_exact(ctx, sva):
 def test_lr_check_2d(ctx, sva, oracle, sx, sy):
     W, H, D = 110, 180, 64
     L, R, _ = synth.stereo_pair2(H, W, D, 0, sx, sy, seed=5, stripes=6, step=9)
-    p = sva.default_params(D=D, dir=sx, dir_y=sy, lr_check=1, lr_max_diff=1)
-    disp, _ = ctx.disparity_sgm(L, R, p)
-    dl, _ = oracle.sgm2(L, R, D, 0, sx, sy, subpixel=False)
+    p = sva.default_params(D=D, dir=sx, dir_y=sy, lr_check=1, lr_max_diff=1, subpixel=1)
+    disp, sub = ctx.disparity_sgm(L, R, p)
+    dl, osub = oracle.sgm2(L, R, D, 0, sx, sy, subpixel=True)
     dr, _ = oracle.sgm2(R, L, D, 0, -sx, -sy, subpixel=False)
     exp = oracle.lr_check2(dl, dr, sx, sy, 1, 0xFFFF)
     assert np.array_equal(disp, exp)
     assert (disp == 0xFFFF).any() and (disp != 0xFFFF).any()
+    assert_sub_close(sub, oracle.lr_sub(exp, osub, 0xFFFF))
 
 
 def _fuse_inputs(n, H, W, seed):

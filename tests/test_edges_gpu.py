@@ -63,3 +63,17 @@ def test_rejects_bad_arguments(ctx, sva):
                dict(D=64, dmin=65500), dict(D=64, P1=-1)):
         with pytest.raises(sva.SvaError):
             ctx.disparity_sgm(L, L, sva.default_params(**kw))
+
+
+def test_rejects_unsupported_shapes(ctx, sva):
+    """shapes the kernels cannot launch are refused before any
+    workspace is allocated: H > 65535 (gridDim.y of the L/R check) and
+    W*H*D >= 2^32 (32-bit path-volume offsets)."""
+    tall = np.zeros((65536, 1), np.uint8)
+    with pytest.raises(sva.SvaError) as e:
+        ctx.disparity_sgm(tall, tall, sva.default_params(D=64))
+    assert e.value.status == sva.SVA_ERR_UNSUPPORTED
+    wide = np.zeros((1024, 16384), np.uint8)           # 16384*1024*256 = 2^32
+    with pytest.raises(sva.SvaError) as e:
+        ctx.disparity_sgm(wide, wide, sva.default_params(D=256))
+    assert e.value.status == sva.SVA_ERR_UNSUPPORTED

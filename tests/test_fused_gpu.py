@@ -15,6 +15,8 @@ import torch
 
 from stereovisionarray_amd import synth
 
+from checks import assert_sub_close
+
 pytestmark = pytest.mark.gpu
 
 
@@ -137,15 +139,40 @@ def test_fused_pipeline(fused_ctx, sva, oracle, W, H, D, dmin, dir):
     assert np.max(np.abs(sub - osub)) <= 1e-5
 
 
-def test_fused_pipeline_lr_check(fused_ctx, sva, oracle):
+# the fused route's L/R pass reuses one padded census buffer with
+# swapped offsets and a flipped step (sva_api.cpp fused_paths), so it is run
+# over D (incl. config 3's 256), both step signs and dmin > 0.
+@pytest.mark.parametrize("D,dir,dmin", [(64, -1, 0), (128, -1, 0), (128, 1, 0), (128, -1, 7),
+                                        (256, -1, 0), (256, 1, 5), (256, -1, 3)])
+def test_fused_pipeline_lr_check(fused_ctx, sva, oracle, D, dir, dmin):
     """The L/R pass swaps the padded census maps' roles inside one buffer."""
-    W, H, D = 180, 60, 64
-    L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=11, stripes=6, step=9)
-    p = sva.default_params(D=D, lr_check=1, lr_max_diff=1, invalid=0xFFFF)
-    disp, _ = fused_ctx.disparity_sgm(L, R, p)
-    dl, _ = oracle.sgm(L, R, D, 0, -1, subpixel=False, threads=8)
-    dr, _ = oracle.sgm(R, L, D, 0, 1, subpixel=False, threads=8)
-    assert np.array_equal(disp, oracle.lr_check(dl, dr, -1, 1, 0xFFFF))
+    W, H = 260, 48
+    L, R, _ = synth.stereo_pair(H, W, D, dmin, dir, seed=11 + D, stripes=6, step=9)
+    p = sva.default_params(D=D, dmin=dmin, dir=dir, lr_check=1, lr_max_diff=1, invalid=0xFFFF,
+                           subpixel=1)
+    disp, sub = fused_ctx.disparity_sgm(L, R, p)
+    dl, osub = oracle.sgm(L, R, D, dmin, dir, subpixel=True, threads=8)
+    dr, _ = oracle.sgm(R, L, D, dmin, -dir, subpixel=False, threads=8)
+    exp = oracle.lr_check(dl, dr, dir, 1, 0xFFFF)
+    assert np.array_equal(disp, exp)
+    assert (disp == 0xFFFF).any() and (disp != 0xFFFF).any()
+    assert_sub_close(sub, oracle.lr_sub(exp, osub, 0xFFFF))
+
+
+@pytest.mark.parametrize("dir", [-1, 1])
+def test_auto_d256_lr_check(ctx, sva, oracle, dir):
+    """A context left on SVA_PATH_KERNEL_AUTO takes the fused route at D=256
+    (DESIGN.md §4.5), L/R check included."""
+    W, H, D, dmin = 300, 40, 256, 2
+    L, R, _ = synth.stereo_pair(H, W, D, dmin, dir, seed=31, stripes=6, step=9)
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
+    p = sva.default_params(D=D, dmin=dmin, dir=dir, lr_check=1, lr_max_diff=1, subpixel=1)
+    disp, sub = ctx.disparity_sgm(L, R, p)
+    dl, osub = oracle.sgm(L, R, D, dmin, dir, subpixel=True, threads=8)
+    dr, _ = oracle.sgm(R, L, D, dmin, -dir, subpixel=False, threads=8)
+    exp = oracle.lr_check(dl, dr, dir, 1, 0xFFFF)
+    assert np.array_equal(disp, exp)
+    assert_sub_close(sub, oracle.lr_sub(exp, osub, 0xFFFF))
 
 
 def test_fused_pipeline_2d_step_uses_cost_volume(fused_ctx, sva, oracle):

@@ -245,6 +245,17 @@ def test_lr_check_kat(oracle):
     assert out[0].tolist() == [0, 0xFFFF, 2, 1]
 
 
+def test_lr_sub_kat(oracle):
+    """the f32 map is NaN exactly where the checked disparity
+    is `invalid`."""
+    d = np.array([[5, 0xFFFF, 7, 0xFFFF]], np.uint16)
+    s = np.array([[5.25, 3.5, 6.75, 1.0]], np.float32)
+    out = oracle.lr_sub(d, s, 0xFFFF)
+    assert np.isnan(out[0, 1]) and np.isnan(out[0, 3])
+    assert out[0, 0] == 5.25 and out[0, 2] == 6.75
+    assert s[0, 1] == 3.5          # input untouched
+
+
 def test_cost2_kat(oracle):
     """2-D step: hand-placed census words."""
     cl = np.zeros((4, 3), np.uint64)

@@ -12,6 +12,8 @@ import torch
 
 from stereovisionarray_amd import synth
 
+from checks import assert_sub_close
+
 pytestmark = pytest.mark.gpu
 
 SUB_TOL = 1e-5
@@ -176,13 +178,16 @@ def test_full_pipeline_device_buffers(ctx, sva, oracle, torch_dev):
 def test_lr_check(ctx, sva, oracle, D, dir, dmin):
     W, H = 300, 60
     L, R, _ = synth.stereo_pair(H, W, D, dmin, dir, seed=11, stripes=6, step=9)
-    p = sva.default_params(D=D, dmin=dmin, dir=dir, lr_check=1, lr_max_diff=1, invalid=0xFFFF)
-    disp, _ = ctx.disparity_sgm(L, R, p)
-    dl, _ = oracle.sgm(L, R, D, dmin, dir, subpixel=False, threads=8)
+    p = sva.default_params(D=D, dmin=dmin, dir=dir, lr_check=1, lr_max_diff=1, invalid=0xFFFF,
+                           subpixel=1)
+    disp, sub = ctx.disparity_sgm(L, R, p)
+    dl, osub = oracle.sgm(L, R, D, dmin, dir, subpixel=True, threads=8)
     dr, _ = oracle.sgm(R, L, D, dmin, -dir, subpixel=False, threads=8)
     exp = oracle.lr_check(dl, dr, dir, 1, 0xFFFF)
     assert np.array_equal(disp, exp)
     assert (disp == 0xFFFF).any() and (disp != 0xFFFF).any()
+    assert_sub_close(sub, oracle.lr_sub(exp, osub, 0xFFFF))
+
 
 
 def test_shifted_texture_exact(ctx, sva):
