@@ -128,9 +128,10 @@ void svo_sgm(const uint8_t* left, const uint8_t* right, int W, int H, ptrdiff_t 
  * |dL - dR(matched)| > max_diff are set to invalid. */
 void svo_lr_check(uint16_t* disp_l, const uint16_t* disp_r, int W, int H, int dir,
                   int max_diff, uint16_t invalid);
+/* The f32 sub-pixel map after the check: NaN wherever disp == invalid. */
+void svo_lr_sub(const uint16_t* disp, float* sub, size_t n, uint16_t invalid);
 /* 2-D form: the right-reference map was computed with (-sx, -sy); the left
  * disparity d is followed to (x, y) + svo_step_offset(d, sx, sy). */
-void svo_lr_sub(const uint16_t* disp, float* sub, size_t n, uint16_t invalid);
 void svo_lr_check2(uint16_t* disp_l, const uint16_t* disp_r, int W, int H, int sx, int sy,
                    int max_diff, uint16_t invalid);
 
