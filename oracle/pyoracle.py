@@ -59,6 +59,8 @@ def _load():
         "svo_wta": (None, [vp, i32, i32, i32, i32, vp, vp]),
         "svo_sgm": (None, [vp, vp, i32, i32, ct.c_ssize_t, i32, i32, i32, i32, i32, vp, vp, i32]),
         "svo_lr_check": (None, [vp, vp, i32, i32, i32, i32, ct.c_uint16]),
+        "svo_sgm2": (None, [vp, vp, i32, i32, ct.c_ssize_t, i32, i32, i32, i32, i32, i32, vp, vp,
+                            i32]),
         "svo_lr_sub": (None, [vp, vp, ct.c_size_t, ct.c_uint16]),
         "svo_step_offset": (None, [i32, i32, i32, P(i32), P(i32)]),
         "svo_shift_perspective": (None, [P(OCamera), P(OCamera), vp, vp, i32, i32,
@@ -235,10 +237,14 @@ def cost2(cl, cr, D, dmin, sx, sy):
 
 def sgm2(left, right, D, dmin=0, sx=-1, sy=0, P1=10, P2=120, subpixel=True, threads=8):
     """Mode S with a 2-D matching step (census -> cost2 -> 8 paths -> WTA)."""
-    cl, cr = census(left), census(right)
-    C = cost2(cl, cr, D, dmin, sx, sy)
-    S = aggregate(C, P1, P2, threads)
-    return wta(S, dmin, subpixel)
+    left = _c(left, np.uint8)
+    right = _c(right, np.uint8)
+    H, W = left.shape
+    disp = np.zeros((H, W), np.uint16)
+    sub = np.zeros((H, W), np.float32) if subpixel else None
+    lib.svo_sgm2(_p(left), _p(right), W, H, W, D, dmin, sx, sy, P1, P2, _p(disp), _p(sub),
+                 threads)
+    return disp, sub
 
 
 def lr_check2(disp_l, disp_r, sx, sy, max_diff=1, invalid=0xFFFF):

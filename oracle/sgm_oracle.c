@@ -78,18 +78,23 @@ void svo_step_offset(int s, int bx, int by, int* ox, int* oy) {
 
 void svo_cost2(const uint64_t* cl, const uint64_t* cr, int W, int H, int D, int dmin, int sx,
                int sy, uint8_t* C) {
-    for (int d = 0; d < D; d++) {
-        int ox, oy;
-        svo_step_offset(dmin + d, sx, sy, &ox, &oy);
-        for (int y = 0; y < H; y++)
-            for (int x = 0; x < W; x++) {
-                int xr = x + ox, yr = y + oy;
+    int* ox = (int*)malloc((size_t)D * sizeof(int));
+    int* oy = (int*)malloc((size_t)D * sizeof(int));
+    for (int d = 0; d < D; d++) svo_step_offset(dmin + d, sx, sy, &ox[d], &oy[d]);
+    #ifdef _OPENMP
+#pragma omp parallel for num_threads(g_threads) schedule(static)
+#endif
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++)
+            for (int d = 0; d < D; d++) {
+                int xr = x + ox[d], yr = y + oy[d];
                 int c = 62;
                 if (xr >= 0 && xr < W && yr >= 0 && yr < H)
                     c = popcount64(cl[(size_t)y * W + x] ^ cr[(size_t)yr * W + xr]);
                 C[((size_t)y * W + x) * D + d] = (uint8_t)c;
             }
-    }
+    free(ox);
+    free(oy);
 }
 
 /* DESIGN.md §2.3 -- direction table r = 0..7 (step vectors p = q + r). */
@@ -129,24 +134,6 @@ void svo_path(const uint8_t* C, int W, int H, int D, int rx, int ry, int P1, int
             }
         }
     }
-}
-
-void svo_aggregate(const uint8_t* C, int W, int H, int D, int P1, int P2, uint16_t* S,
-                   int threads) {
-    size_t n = (size_t)W * H * D;
-    memset(S, 0, n * sizeof(uint16_t));
-    uint8_t* L = (uint8_t*)malloc(n);
-    for (int r = 0; r < 8; r++) {
-        int rx, ry;
-        svo_direction(r, &rx, &ry);
-        svo_path(C, W, H, D, rx, ry, P1, P2, L);
-        (void)threads;
-#ifdef _OPENMP
-#pragma omp parallel for num_threads(threads > 1 ? threads : 1) schedule(static)
-#endif
-        for (long long i = 0; i < (long long)n; i++) S[i] = (uint16_t)(S[i] + L[i]);
-    }
-    free(L);
 }
 
 /* DESIGN.md §2.4 -- first-minimum WTA (mirrors CameraStereoVision.cpp:85)
@@ -222,6 +209,49 @@ static void svo_path_threaded(const uint8_t* C, int W, int H, int D, int rx, int
         for (; x >= 0 && x < W && y >= 0 && y < H; x += rx, y += ry)
             path_line_step(C, L, W, H, D, x, y, rx, ry, P1, P2);
     }
+}
+
+/* S = sum of the 8 path volumes; threads > 1 walks each direction's lines in
+ * parallel (svo_path_threaded), same arithmetic as the serial svo_path. */
+void svo_aggregate(const uint8_t* C, int W, int H, int D, int P1, int P2, uint16_t* S,
+                   int threads) {
+    size_t n = (size_t)W * H * D;
+    memset(S, 0, n * sizeof(uint16_t));
+    uint8_t* L = (uint8_t*)malloc(n);
+    for (int r = 0; r < 8; r++) {
+        int rx, ry;
+        svo_direction(r, &rx, &ry);
+        if (threads > 1) svo_path_threaded(C, W, H, D, rx, ry, P1, P2, L, threads);
+        else svo_path(C, W, H, D, rx, ry, P1, P2, L);
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(threads > 1 ? threads : 1) schedule(static)
+#endif
+        for (long long i = 0; i < (long long)n; i++) S[i] = (uint16_t)(S[i] + L[i]);
+    }
+    free(L);
+}
+
+/* Whole Mode S pipeline on a 2-D matching step: census ->
+ * svo_cost2 -> 8 paths -> WTA; threads <= 1: serial. */
+void svo_sgm2(const uint8_t* left, const uint8_t* right, int W, int H, ptrdiff_t pitch, int D,
+              int dmin, int sx, int sy, int P1, int P2, uint16_t* disp, float* sub,
+              int threads) {
+    size_t np = (size_t)W * H, n = np * D;
+    uint64_t* cl = (uint64_t*)malloc(np * 8);
+    uint64_t* cr = (uint64_t*)malloc(np * 8);
+    uint8_t* C = (uint8_t*)malloc(n);
+    uint16_t* S = (uint16_t*)malloc(n * 2);
+    g_threads = threads > 1 ? threads : 1;
+    svo_census(left, W, H, pitch, cl);
+    svo_census(right, W, H, pitch, cr);
+    svo_cost2(cl, cr, W, H, D, dmin, sx, sy, C);
+    svo_aggregate(C, W, H, D, P1, P2, S, threads);
+    svo_wta(S, W, H, D, dmin, disp, sub);
+    g_threads = 1;
+    free(cl);
+    free(cr);
+    free(C);
+    free(S);
 }
 
 void svo_sgm(const uint8_t* left, const uint8_t* right, int W, int H, ptrdiff_t pitch, int D,

@@ -123,6 +123,11 @@ void svo_wta(const uint16_t* S, int W, int H, int D, int dmin, uint16_t* disp, f
 void svo_sgm(const uint8_t* left, const uint8_t* right, int W, int H, ptrdiff_t pitch, int D,
              int dmin, int dir, int P1, int P2, uint16_t* disp, float* sub, int threads);
 
+/* Mode S on a 2-D matching step (svo_cost2); threads <= 1: serial. */
+void svo_sgm2(const uint8_t* left, const uint8_t* right, int W, int H, ptrdiff_t pitch, int D,
+              int dmin, int sx, int sy, int P1, int P2, uint16_t* disp, float* sub,
+              int threads);
+
 /* Left/right consistency check.  disp_r is the disparity map
  * computed with the roles of the images swapped (dir negated); pixels whose
  * |dL - dR(matched)| > max_diff are set to invalid. */

@@ -163,3 +163,47 @@ def test_ref_path_full_frame_vga(ctx, sva, oracle, pair):
     d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k)
     o8, o16, ov, _ = oracle.ref_pair(a, b, ocr, oco, k=k)
     assert np.array_equal(valid, ov) and np.array_equal(d16, o16) and np.array_equal(d8, o8)
+
+
+# VERDICT r01 "next" #2: the offset-plane kernel's tiling, LDS bitmap and
+# per-tile fallback at the headline size.  32 full-width rows spread from top
+# to bottom (so every 32-row tile band is entered at a different row) keep the
+# CPU restatement to a few seconds; the oracle runs over row chunks in
+# threads (ctypes drops the GIL; each call writes only its own masked pixels).
+MODE_R_1080P_ROWS = np.linspace(20, 1080 - 21, 32).astype(int)
+
+
+def _oracle_rows(oracle, a, b, ocr, oco, k, rows, W, H, chunks=16):
+    from concurrent.futures import ThreadPoolExecutor
+    o8 = np.zeros((H, W), np.uint8)
+    o16 = np.zeros((H, W), np.uint16)
+    ov = np.zeros((H, W), np.uint8)
+
+    def part(rs):
+        m = np.zeros((H, W), np.uint8)
+        m[rs, :] = 1
+        oracle.ref_pair(a, b, ocr, oco, k=k, mask=m, disp_u8=o8, disp_u16=o16, valid=ov)
+
+    with ThreadPoolExecutor(chunks) as ex:
+        list(ex.map(part, np.array_split(rows, chunks)))
+    return o8, o16, ov
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("pair", [(12, 11), (12, 7), (12, 18), (12, 6)])
+def test_ref_path_1080p_row_sampled(ctx, sva, oracle, pair):
+    W, H, k = 1920, 1080, 20
+    cr, co, ocr, oco = cams_for(sva, oracle, W, *pair)
+    a = synth.texture(H, W, 40 + pair[1])
+    # the other camera sees the scene shifted by ~178 px per grid unit
+    # (0.05 m * 0.05 m / 0.75 m / (0.036 / 1920) m/px) along its baseline
+    gx, gy = pair[1] % 5 - 2, pair[1] // 5 - 2
+    b = np.roll(np.roll(a, -178 * gy, axis=0), -178 * gx, axis=1)
+    mask = np.zeros((H, W), np.uint8)
+    mask[MODE_R_1080P_ROWS, :] = 1
+    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k, mask=mask)
+    o8, o16, ov = _oracle_rows(oracle, a, b, ocr, oco, k, MODE_R_1080P_ROWS, W, H)
+    assert ov.sum() > 0.3 * mask.sum()
+    assert np.array_equal(valid, ov)
+    assert np.array_equal(d16, o16)
+    assert np.array_equal(d8, o8)
