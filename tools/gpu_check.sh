@@ -16,9 +16,9 @@ run() {
 for step in "$@"; do
   case "$step" in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) run pytest_gpu 1200 python -m pytest tests -q -m "gpu and not slow" -x ;;
-    pytest_all) run pytest_gpu_all 1500 python -m pytest tests -q -m gpu ;;
-    pytest_slow) run pytest_gpu_slow 900 python -m pytest tests -q -m "gpu and slow" ;;
+    pytest) run pytest_gpu 1200 python -u -m pytest tests -q -m "gpu and not slow" -x --timeout 120 --timeout-method thread ;;
+    pytest_all) run pytest_gpu_all 1500 python -u -m pytest tests -q -m gpu -rf --timeout 300 --timeout-method thread ;;
+    pytest_slow) run pytest_gpu_slow 900 python -u -m pytest tests -v -m "gpu and slow" -rf --timeout 300 --timeout-method thread ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     pytest_array) run pytest_array 900 python -m pytest tests/test_array_gpu.py -q -m gpu ;;
     array) run center8 600 python bench.py --workload center8 --steps 5 --warmup 2 --no-cpu-baseline
