@@ -155,6 +155,18 @@ int sva_paths_fused_d(void* ctx, const uint8_t* left, const uint8_t* right, int 
                       int height, size_t pitch, const sva_sgm_params* p, uint8_t* L8);
 int sva_aggregate_d(void* ctx, const uint8_t* C, int width, int height,
                     const sva_sgm_params* p, uint16_t* S);
+/* Checkpoint-mode stages of the cost-volume frame pipeline.
+ * sva_paths_ckpt_d: L6 = [6][H][W][D] u8, the volumes of directions 2..7 (same
+ * values as slots 2..7 of sva_paths_d); CK = [2][H][ns][D] u8, the horizontal
+ * states: CK[0][y][s] = L_0(s*seg + seg - 1, y), CK[1][y][s] = L_1(s*seg, y)
+ * (entries with no such column are not written).  sva_wta_h_d recomputes the
+ * two horizontal directions per segment from CK and finishes S, WTA and the
+ * sub-pixel map.  seg and ns from sva_ckpt_segments (no device needed). */
+int sva_ckpt_segments(int width, int D, int* ns, int* seg);
+int sva_paths_ckpt_d(void* ctx, const uint8_t* C, int width, int height, const sva_sgm_params* p,
+                     uint8_t* L6, uint8_t* CK);
+int sva_wta_h_d(void* ctx, const uint8_t* C, const uint8_t* L6, const uint8_t* CK, int width,
+                int height, const sva_sgm_params* p, uint16_t* disp, float* subpix);
 int sva_wta_d(void* ctx, const uint16_t* S, int width, int height, const sva_sgm_params* p,
               uint16_t* disp, float* subpix);
 

@@ -48,7 +48,8 @@ EXPORTED = [
     "sva_points_to_depth_d", "sva_points_to_depth", "sva_depth_to_points_d",
     "sva_depth_to_points", "sva_resize_half_size", "sva_resize_half_d", "sva_resize_half",
     "sva_batch_sgm", "sva_resize_linear_f64_d", "sva_resize_linear_f64", "sva_ref_error_d",
-    "sva_ref_error", "sva_masked_mean_d", "sva_masked_mean",
+    "sva_ref_error", "sva_masked_mean_d", "sva_masked_mean", "sva_ckpt_segments",
+    "sva_paths_ckpt_d", "sva_wta_h_d",
 ]
 
 
@@ -137,6 +138,9 @@ def _load() -> ct.CDLL:
         "sva_census_cost_d": (i32, [vp, vp, vp, i32, i32, sz, P(SgmParams), vp]),
         "sva_aggregate_d": (i32, [vp, vp, i32, i32, P(SgmParams), vp]),
         "sva_wta_d": (i32, [vp, vp, i32, i32, P(SgmParams), vp, vp]),
+        "sva_ckpt_segments": (i32, [i32, i32, P(i32), P(i32)]),
+        "sva_paths_ckpt_d": (i32, [vp, vp, i32, i32, P(SgmParams), vp, vp]),
+        "sva_wta_h_d": (i32, [vp, vp, vp, vp, i32, i32, P(SgmParams), vp, vp]),
         "sva_disparity_ref": (i32, [vp, vp, vp, i32, i32, sz, vp, P(Camera), P(Camera), i32,
                                     dbl, dbl, vp, vp, vp]),
         "sva_disparity_ref_d": (i32, [vp, vp, vp, i32, i32, sz, vp, P(Camera), P(Camera), i32,
@@ -193,6 +197,15 @@ def resize_half_size(W: int, H: int):
     if lib.sva_resize_half_size(W, H, ct.byref(dw), ct.byref(dh)) != 0:
         raise ValueError("bad size")
     return dw.value, dh.value
+
+
+def ckpt_segments(W: int, D: int):
+    """(ns, seg) of the horizontal checkpoint layout (sva_ckpt_segments)."""
+    ns, seg = ct.c_int(), ct.c_int()
+    st = lib.sva_ckpt_segments(W, D, ct.byref(ns), ct.byref(seg))
+    if st:
+        raise SvaError(st, "sva_ckpt_segments")
+    return ns.value, seg.value
 
 
 def device_count() -> int:
@@ -305,6 +318,13 @@ class Context:
 
     def aggregate_d(self, C, W, H, params, S):
         self._chk(lib.sva_aggregate_d(self.h, _ptr(C), W, H, ct.byref(params), _ptr(S)))
+
+    def paths_ckpt_d(self, C, W, H, params, L6, CK):
+        self._chk(lib.sva_paths_ckpt_d(self.h, _ptr(C), W, H, ct.byref(params), _ptr(L6), _ptr(CK)))
+
+    def wta_h_d(self, C, L6, CK, W, H, params, disp, sub=None):
+        self._chk(lib.sva_wta_h_d(self.h, _ptr(C), _ptr(L6), _ptr(CK), W, H, ct.byref(params),
+                                  _ptr(disp), _ptr(sub)))
 
     def wta_d(self, S, W, H, params, disp, sub=None):
         self._chk(lib.sva_wta_d(self.h, _ptr(S), W, H, ct.byref(params), _ptr(disp), _ptr(sub)))

@@ -30,8 +30,21 @@ struct PathGeom {
     int blk_h;    // blocks per horizontal direction (H lines)
     int blk_w;    // blocks per vertical / diagonal direction (W lines)
     size_t vol;   // bytes of one direction volume (W*H*D)
-    int store_aux; // cache-policy bits for the path stores (0 = default)
+    int ckpt;     // 1: horizontal lines store only segment checkpoints (below)
+    int ns;       // checkpoint segments per row, ceil(W / kSeg)
+    size_t ckvol; // bytes of one direction's checkpoint plane (H*ns*D)
 };
+
+// Horizontal-line checkpoints.  With g.ckpt set, the two
+// horizontal directions write no L_r volume: direction 0 (left to right)
+// stores L(x) at the last column of every seg-wide segment but the row's
+// last, direction 1 (right to left) at the first column of every segment but
+// the first; [2][H][ns][D] u8.  The WTA kernel (wta_h.hip) re-runs both
+// recurrences segment by segment from these states, so their L_r bytes never
+// reach HBM.  seg = 32 columns up to D = 128 and 16 above: wta_h keeps a
+// segment's left-to-right L in registers, seg * D/64 dwords per lane.
+template <int DPL> constexpr int seg_log2() { return DPL <= 8 ? 5 : 4; }
+inline int seg_log2_of(int D) { return D <= 128 ? 5 : 4; }
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
@@ -77,33 +90,25 @@ __device__ __forceinline__ Words<NW> bload(rsrc_t r, unsigned off) {
     return o;
 }
 
-// VAR (ablation builds only, -DSVA_PATHS_ABLATION): 2 = no stores,
-// 3 = no loads, 4 = neither.  Production code is VAR = 0.
-template <int NW, int VAR>
-__device__ __forceinline__ void bstore(rsrc_t r, unsigned off, const unsigned (&w)[NW], int aux) {
+// VAR (experiment builds only, csrc/experiments/): 2 = no stores,
+// 3 = no loads, 4 = neither.  Production code is VAR = 0.  AUX = cache-policy
+// bits of the store (kStoreNT for the streamed L_r volumes).
+template <int NW, int VAR, int AUX = kStoreNT>
+__device__ __forceinline__ void bstore(rsrc_t r, unsigned off, const unsigned (&w)[NW]) {
     if constexpr (VAR == 2 || VAR == 4) {
 #pragma unroll
         for (int i = 0; i < NW; i++) asm volatile("" ::"v"(w[i]));
-    } else if constexpr (VAR == 9) {
-        typedef unsigned v2u __attribute__((ext_vector_type(2)));
-        switch (aux) {
-            case 2: __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, r, off, 0, 2); break;
-            case 16: __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, r, off, 0, 16); break;
-            case 18: __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, r, off, 0, 18); break;
-            case 17: __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, r, off, 0, 17); break;
-            default: __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, r, off, 0, 0); break;
-        }
     } else if constexpr (NW == 1) {
-        __builtin_amdgcn_raw_buffer_store_b32(w[0], r, off, 0, kStoreNT);
+        __builtin_amdgcn_raw_buffer_store_b32(w[0], r, off, 0, AUX);
     } else if constexpr (NW == 2) {
         typedef unsigned v2u __attribute__((ext_vector_type(2)));
-        __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, r, off, 0, kStoreNT);
+        __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, r, off, 0, AUX);
     } else if constexpr (NW == 3) {
         typedef unsigned v3u __attribute__((ext_vector_type(3)));
-        __builtin_amdgcn_raw_buffer_store_b96((v3u){w[0], w[1], w[2]}, r, off, 0, kStoreNT);
+        __builtin_amdgcn_raw_buffer_store_b96((v3u){w[0], w[1], w[2]}, r, off, 0, AUX);
     } else {
         typedef unsigned v4u __attribute__((ext_vector_type(4)));
-        __builtin_amdgcn_raw_buffer_store_b128((v4u){w[0], w[1], w[2], w[3]}, r, off, 0, kStoreNT);
+        __builtin_amdgcn_raw_buffer_store_b128((v4u){w[0], w[1], w[2], w[3]}, r, off, 0, AUX);
     }
 }
 
@@ -245,17 +250,13 @@ template <int DPL> constexpr int pf_v() {
     return DPL == 4 ? SVA_PF_V4 : DPL == 8 ? SVA_PF_V8 : DPL == 12 ? SVA_PF_V12 : SVA_PF_V16;
 }
 
-#ifdef SVA_PATHS_TRACE
-// Experiment builds only: per-wave s_memrealtime stamps every 96 steps
-// (tools/paths_trace.py), [wave][0] = direction, [wave][1 + t/96] = stamp.
-__device__ unsigned long long* g_paths_trace;
-constexpr int kTraceSlots = 32;
-#endif
 
-// One path line over a materialised cost volume C.
-template <int DPL, bool DIAG, int VAR, int PF>
+// One path line over a materialised cost volume C.  CKPT
+// (horizontal lines only): store segment checkpoints to rCK instead of the
+// full L_r line to rL.
+template <int DPL, bool DIAG, int VAR, int PF, bool CKPT = false>
 __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& g, int rx, int ry,
-                                          int line, int k) {
+                                          int line, int k, rsrc_t rCK) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
     const int W = g.W, H = g.H, D = g.D;
     const unsigned P1 = (unsigned)g.P1, P2 = (unsigned)g.P2;
@@ -295,13 +296,24 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
     // values never overlap and the slot keeps its registers: no copies, and
     // every wait is for a load issued ~PF steps earlier.  (Refilling first
     // made hipcc copy the whole ring at the loop head behind vmcnt(1..3).)
-    auto step = [&](int p, bool refill) {
+    auto step = [&](int p, bool refill, int ts) {
         unsigned cw[NW];
 #pragma unroll
         for (int w = 0; w < NW; w++) cw[w] = ring[p].w[w];
         unsigned ow[NW];
         sgm_step<DPL>(cw, A, m, ow, P1, P2);
-        bstore<NW, VAR>(rL, cc.off, ow, g.store_aux);
+        if constexpr (CKPT) {
+            // ts is the (wave-uniform) step index; x the pixel just computed
+            const int x = rx > 0 ? ts : W - 1 - ts;
+            constexpr int SL = seg_log2<DPL>(), SEG = 1 << SL;
+            const bool hit = rx > 0 ? (((x + 1) & (SEG - 1)) == 0 && x + 1 < W)
+                                    : ((x & (SEG - 1)) == 0 && x > 0);
+            if (hit)   // default policy: the WTA kernel reads these back soon
+                bstore<NW, VAR, 0>(rCK, ((unsigned)(y0 * g.ns + (x >> SL)) * (unsigned)D +
+                                         (unsigned)(k * DPL)), ow);
+        } else {
+            bstore<NW, VAR>(rL, cc.off, ow);
+        }
         const bool wrapped = cc.advance(rx, stride, W, WD);
         if constexpr (DIAG) {   // restart where x wraps: selects, no divergent branch
 #pragma unroll
@@ -322,23 +334,14 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
     };
 
     int t = 0;
-#ifdef SVA_PATHS_TRACE
-    const unsigned wid = blockIdx.x * 4 + (threadIdx.x >> 6);
-    unsigned long long* tr = g_paths_trace + (size_t)wid * kTraceSlots;
-    const bool rec = (threadIdx.x & 63) == 0;
-    if (rec) tr[0] = (unsigned long long)(10 + (rx + 1) * 3 + (ry + 1));
-#endif
     for (; t + PF <= steps; t += PF) {
-#ifdef SVA_PATHS_TRACE
-        if (rec && t % 96 == 0 && 1 + t / 96 < kTraceSlots) tr[1 + t / 96] = __builtin_amdgcn_s_memrealtime();
-#endif
 #pragma unroll
-        for (int p = 0; p < PF; p++) step(p, true);
+        for (int p = 0; p < PF; p++) step(p, true, t + p);
     }
     // tail: fewer than PF steps left, all already in the ring
 #pragma unroll
     for (int p = 0; p < PF; p++)
-        if (t + p < steps) step(p, false);
+        if (t + p < steps) step(p, false, t + p);
 }
 
 

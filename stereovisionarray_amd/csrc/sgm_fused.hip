@@ -190,7 +190,7 @@ __device__ __forceinline__ void fused_h(rsrc_t rC, rsrc_t rL, const FusedGeom& g
         }
         unsigned ow[NW];
         sgm_step_c<DPL>(c, A, m, ow, P1, P2);
-        bstore<NW, 0>(rL, soff, ow, 0);
+        bstore<NW, 0>(rL, soff, ow);
         soff += sstride;
     };
 
@@ -336,7 +336,7 @@ __device__ __forceinline__ void fused_vd(rsrc_t rC, rsrc_t rL, const FusedGeom& 
         }
         unsigned ow[NW];
         sgm_step_c<DPL>(c, A, m, ow, P1, P2);
-        bstore<NW, 0>(rL, live ? cc.off : g.vol, ow, 0);   // phantom line: past the range, dropped
+        bstore<NW, 0>(rL, live ? cc.off : g.vol, ow);   // phantom line: past the range, dropped
         const bool wrapped = cc.advance(rx, sstride, W, WD);
         if constexpr (DIAG) {
 #pragma unroll

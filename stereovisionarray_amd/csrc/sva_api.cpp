@@ -215,58 +215,68 @@ int run_sgm_fused(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int 
     return SVA_OK;
 }
 
+size_t ckpt_bytes(int W, int H, int D) { return 2 * (size_t)H * ckpt_segments(W, D) * (size_t)D; }
+
+// Paths + WTA of the cost-volume frame pipeline: sgm_paths
+// in checkpoint mode (6 volumes + horizontal checkpoints), then wta_h, which
+// recomputes the two horizontal directions per segment and picks d*.
+int paths_wta(Ctx* c, const uint8_t* C, int W, int H, const sva_sgm_params* p, uint16_t* disp,
+              float* sub) {
+    const size_t nv = (size_t)W * H * (size_t)p->D;
+    SVA_HIP(c, c->paths.ensure(nv * 6), "path workspace");
+    SVA_HIP(c, c->ckpt.ensure(ckpt_bytes(W, H, p->D)), "checkpoint workspace");
+    uint8_t* L6 = (uint8_t*)c->paths.ptr;
+    uint8_t* CK = (uint8_t*)c->ckpt.ptr;
+    SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L6, CK), "paths launch");
+    SVA_HIP(c, launch_wta_h(*c, C, L6, CK, W, H, p->D, p->P1, p->P2, p->dmin, disp, sub),
+            "wta launch");
+    return SVA_OK;
+}
+
 // Mode S on device buffers: census -> cost -> 8 paths -> WTA (-> L/R check).
 int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int H, size_t pitch,
                    const sva_sgm_params* p, uint16_t* disp, float* sub) {
     if (use_fused(c, p, W, H)) return run_sgm_fused(c, left, right, W, H, pitch, p, disp, sub);
     const size_t np = (size_t)W * H, nv = np * (size_t)p->D;
+    int s;
+    SVA_HIP(c, c->cost.ensure(nv), "cost workspace");
+    uint8_t* C = (uint8_t*)c->cost.ptr;
+    uint16_t* dr = nullptr;
+    if (p->lr_check) {
+        SVA_HIP(c, c->disp_r.ensure(np * 2), "lr workspace");
+        dr = (uint16_t*)c->disp_r.ptr;
+    }
     if (p->dir_y == 0 && p->D >= 128 && census_cost_supported(p->D) && !c->split_census) {
         // census maps stay on chip: one census+cost kernel (census_cost.hip),
         // once per matching role when the L/R check runs.
         // In-process A/B per frame at 1080p: D=128 1.129 -> 1.112 ms,
         // D=192 1.646 -> 1.588 ms; D=64 is faster split (0.609 vs 0.650 ms).
-        SVA_HIP(c, c->cost.ensure(nv), "cost workspace");
-        SVA_HIP(c, c->paths.ensure(nv * 8), "path workspace");
-        uint8_t* C = (uint8_t*)c->cost.ptr;
-        uint8_t* L8 = (uint8_t*)c->paths.ptr;
         SVA_HIP(c, launch_census_cost(*c, left, right, W, H, pitch, p->D, p->dmin, p->dir, C),
                 "cost launch");
-        SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
-        SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, disp, sub), "wta launch");
+        if ((s = paths_wta(c, C, W, H, p, disp, sub))) return s;
         if (p->lr_check) {
             // right image as reference: the images swap roles, the step flips
-            SVA_HIP(c, c->disp_r.ensure(np * 2), "lr workspace");
-            uint16_t* dr = (uint16_t*)c->disp_r.ptr;
             SVA_HIP(c, launch_census_cost(*c, right, left, W, H, pitch, p->D, p->dmin, -p->dir, C),
                     "cost launch");
-            SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
-            SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, dr, nullptr),
-                    "wta launch");
-            SVA_HIP(c, launch_lr_check(*c, disp, dr, sub, W, H, p->dir, 0, p->lr_max_diff, p->invalid),
+            if ((s = paths_wta(c, C, W, H, p, dr, nullptr))) return s;
+            SVA_HIP(c, launch_lr_check(*c, disp, dr, sub, W, H, p->dir, 0, p->lr_max_diff,
+                                       p->invalid),
                     "lr launch");
         }
         return SVA_OK;
     }
     SVA_HIP(c, c->census_l.ensure(np * 8), "census workspace");
     SVA_HIP(c, c->census_r.ensure(np * 8), "census workspace");
-    SVA_HIP(c, c->cost.ensure(nv), "cost workspace");
-    SVA_HIP(c, c->paths.ensure(nv * 8), "path workspace");
     uint64_t* cl = (uint64_t*)c->census_l.ptr;
     uint64_t* cr = (uint64_t*)c->census_r.ptr;
-    uint8_t* C = (uint8_t*)c->cost.ptr;
-    uint8_t* L8 = (uint8_t*)c->paths.ptr;
     SVA_HIP(c, launch_census_pair(*c, left, right, W, H, pitch, cl, cr), "census launch");
     SVA_HIP(c, launch_cost2(*c, cl, cr, W, H, p->D, p->dmin, p->dir, p->dir_y, C), "cost launch");
-    SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
-    SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, disp, sub), "wta launch");
+    if ((s = paths_wta(c, C, W, H, p, disp, sub))) return s;
     if (p->lr_check) {
-        SVA_HIP(c, c->disp_r.ensure(np * 2), "lr workspace");
-        uint16_t* dr = (uint16_t*)c->disp_r.ptr;
         // right image as reference: roles of the census maps swap, the step flips
         SVA_HIP(c, launch_cost2(*c, cr, cl, W, H, p->D, p->dmin, -p->dir, -p->dir_y, C),
                 "cost launch");
-        SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
-        SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, dr, nullptr), "wta launch");
+        if ((s = paths_wta(c, C, W, H, p, dr, nullptr))) return s;
         SVA_HIP(c, launch_lr_check(*c, disp, dr, sub, W, H, p->dir, p->dir_y, p->lr_max_diff,
                                    p->invalid),
                 "lr launch");
@@ -411,9 +421,6 @@ int sva_create(int device, void** out) {
         return SVA_ERR_DEVICE;
     }
     c->stream = c->own_stream;
-#ifdef SVA_PATHS_MALLOC_FLAGS   // A/B builds only: allocation flags of the path volumes
-    c->paths.flags = SVA_PATHS_MALLOC_FLAGS;
-#endif
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->cu_count = prop.multiProcessorCount;
     *out = c;
@@ -425,7 +432,7 @@ int sva_destroy(void* ctx) {
     if (!c) return SVA_ERR_INVALID_ARG;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->census_l, &c->census_r, &c->cost, &c->paths, &c->scratch_u16,
+    for (DevBuf* b : {&c->census_l, &c->census_r, &c->cost, &c->paths, &c->ckpt, &c->scratch_u16,
                       &c->disp_r, &c->in_a, &c->in_b, &c->in_mask, &c->out_a, &c->out_b,
                       &c->out_c, &c->in_c, &c->shifted, &c->keys, &c->counts, &c->total})
         b->release();
@@ -464,6 +471,7 @@ int sva_reserve(void* ctx, int W, int H, int D) {
     SVA_HIP(c, c->census_r.ensure(np * 8), "reserve");
     SVA_HIP(c, c->cost.ensure(nv), "reserve");
     SVA_HIP(c, c->paths.ensure(nv * 8), "reserve");
+    SVA_HIP(c, c->ckpt.ensure(ckpt_bytes(W, H, D)), "reserve");
     return SVA_OK;
 }
 
@@ -628,6 +636,38 @@ int sva_aggregate_d(void* ctx, const uint8_t* C, int W, int H, const sva_sgm_par
     uint8_t* L8 = (uint8_t*)c->paths.ptr;
     SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
     SVA_HIP(c, launch_sum(*c, L8, W, H, p->D, S), "sum launch");
+    return SVA_OK;
+}
+
+int sva_ckpt_segments(int W, int D, int* ns, int* seg) {
+    if (W <= 0 || !paths_supported(D) || !ns || !seg) return SVA_ERR_INVALID_ARG;
+    *ns = ckpt_segments(W, D);
+    *seg = 1 << sgm_seg_log2(D);
+    return SVA_OK;
+}
+
+int sva_paths_ckpt_d(void* ctx, const uint8_t* C, int W, int H, const sva_sgm_params* p,
+                     uint8_t* L6, uint8_t* CK) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_sgm(c, p, W, H))) return s;
+    if (!C || !L6 || !CK || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
+    SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L6, CK), "paths launch");
+    return SVA_OK;
+}
+
+int sva_wta_h_d(void* ctx, const uint8_t* C, const uint8_t* L6, const uint8_t* CK, int W, int H,
+                const sva_sgm_params* p, uint16_t* disp, float* sub) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    int s;
+    if ((s = check_sgm(c, p, W, H))) return s;
+    if (!C || !L6 || !CK || !disp || W <= 0 || H <= 0)
+        return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
+    SVA_HIP(c, launch_wta_h(*c, C, L6, CK, W, H, p->D, p->P1, p->P2, p->dmin, disp,
+                            p->subpixel ? sub : nullptr),
+            "wta launch");
     return SVA_OK;
 }
 

@@ -57,7 +57,7 @@ struct Ctx {
     std::string last_error;
     KernelTimer timer;
     // Mode S workspace
-    DevBuf census_l, census_r, cost, paths, scratch_u16, disp_r;
+    DevBuf census_l, census_r, cost, paths, ckpt, scratch_u16, disp_r;
     // host-pointer staging
     DevBuf in_a, in_b, in_mask, out_a, out_b, out_c;
     // refinement / 3-D workspace (refine.hip)
@@ -137,10 +137,17 @@ hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right,
                               size_t pitch, int D, int dmin, int dir, uint8_t* C);
 hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,
                        int dmin, int dir, uint8_t* C);
-// sgm_paths.hip -- all 8 directions in one launch; L8 = [8][H][W][D] u8.
+// sgm_paths.hip -- all 8 directions in one launch.  CK == nullptr: L8 =
+// [8][H][W][D] u8.  CK set (checkpoint mode): L8 = [6][H][W][D]
+// (directions 2..7) and CK = [2][H][ckpt_segments(W, D)][D] horizontal states.
 hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
-                        uint8_t* L8);
+                        uint8_t* L8, uint8_t* CK = nullptr);
 bool paths_supported(int D);
+int ckpt_segments(int W, int D);
+int sgm_seg_log2(int D);
+// wta_h.hip -- horizontal recompute from the checkpoints + sum + WTA.
+hipError_t launch_wta_h(Ctx& c, const uint8_t* C, const uint8_t* L6, const uint8_t* CK, int W,
+                        int H, int D, int P1, int P2, int dmin, uint16_t* disp, float* sub);
 // sgm_fused.hip -- the same 8 path volumes computed straight from the census
 // maps (1-D steps, dir = +-1), no cost volume.  cen = padded census buffer,
 // map_l / map_r = word offsets of the reference / matched map inside it.

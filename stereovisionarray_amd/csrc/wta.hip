@@ -3,12 +3,13 @@
 //
 // Same lane layout as sgm_paths.hip: one 16-lane DPP row per pixel, lane k
 // holds disparities [k*DPL, k*DPL+DPL).  S = sum of the 8 u8 path volumes is
-// formed in packed u16 (no carry: S <= 8*255 < 2^16), the first minimum is a
-// u32 min over keys (S << 16 | d) -- the smaller d wins ties, mirroring
-// std::min_element at CameraStereoVision.cpp:85 -- reduced across the row by
-// DPP.  S(d*-1), S(d*+1) for the parabola are fetched with a DPP OR-reduce.
+// formed in packed u16 (no carry: S <= 8*255 < 2^16); the pick is
+// wta_common.h's.  These kernels serve the stage API (sva_wta_d,
+// sva_aggregate_d) and the census-fused route; the cost-volume frame
+// pipeline uses wta_h.hip, which also recomputes the horizontal paths.
 #include "sva_device.h"
 #include "sva_internal.h"
+#include "wta_common.h"
 
 #include <cstdlib>
 
@@ -17,14 +18,6 @@ namespace {
 
 constexpr int BLOCK = 256;
 constexpr int PIX_PER_BLOCK = BLOCK / 16;
-
-__device__ __forceinline__ unsigned row_or_u32(unsigned v) {
-    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_QUAD_1032, 0xf, 0xf, false);
-    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_QUAD_2301, 0xf, 0xf, false);
-    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_HALF_MIRROR, 0xf, 0xf, false);
-    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_MIRROR, 0xf, 0xf, false);
-    return v;
-}
 
 template <int NW>
 __device__ __forceinline__ void load_nw(const uint8_t* p, unsigned (&w)[NW]) {
@@ -42,11 +35,7 @@ __device__ __forceinline__ void load_nw(const uint8_t* p, unsigned (&w)[NW]) {
     }
 }
 
-#ifdef SVA_PATHS_ABLATION
-__constant__ int g_wta_nt = 1;
-#endif
-
-// Last-use reads of the path volumes: non-temporal (ablation: SVA_WTA_NT=0).
+// Last-use reads of the path volumes: non-temporal.
 template <int NW>
 __device__ __forceinline__ void load_nw_nt(const uint8_t* p, unsigned (&w)[NW]) {
     const unsigned* q = (const unsigned*)p;
@@ -71,18 +60,8 @@ __device__ __forceinline__ void sum_paths(const uint8_t* p, size_t vol, unsigned
 #pragma unroll
     for (int j = 0; j < NP; j++) S[j] = 0u;
     unsigned w[8][NW];
-#ifdef SVA_PATHS_ABLATION
-    if (g_wta_nt) {
-#pragma unroll
-        for (int r = 0; r < 8; r++) load_nw_nt<NW>(p + (size_t)r * vol, w[r]);
-    } else {
-#pragma unroll
-        for (int r = 0; r < 8; r++) load_nw<NW>(p + (size_t)r * vol, w[r]);
-    }
-#else
 #pragma unroll
     for (int r = 0; r < 8; r++) load_nw_nt<NW>(p + (size_t)r * vol, w[r]);
-#endif
 #pragma unroll
     for (int r = 0; r < 8; r++)
 #pragma unroll
@@ -97,38 +76,8 @@ __device__ __forceinline__ void sum_paths(const uint8_t* p, size_t vol, unsigned
 template <int DPL>
 __device__ __forceinline__ void wta_finish(const unsigned (&S)[DPL / 2], int k, int D, int dmin,
                                            size_t pix, uint16_t* disp, float* sub) {
-    constexpr int NP = DPL / 2;
-    const int d0 = k * DPL;
-    unsigned best = 0xffffffffu;
-#pragma unroll
-    for (int j = 0; j < NP; j++) {
-        unsigned lo = ((S[j] & 0xffffu) << 16) | (unsigned)(d0 + 2 * j);
-        unsigned hi = (S[j] & 0xffff0000u) | (unsigned)(d0 + 2 * j + 1);
-        best = best < lo ? best : lo;
-        best = best < hi ? best : hi;
-    }
-    best = row_min_u32(best);
-    const int ds = (int)(best & 0xffffu);
-    float v = (float)(dmin + ds);
-    if (sub) {
-        unsigned vm = 0, vp = 0;
-#pragma unroll
-        for (int j = 0; j < NP; j++) {
-            const int da = d0 + 2 * j;
-            const unsigned lo = S[j] & 0xffffu, hi = S[j] >> 16;
-            vm = (da == ds - 1) ? lo : vm;
-            vm = (da + 1 == ds - 1) ? hi : vm;
-            vp = (da == ds + 1) ? lo : vp;
-            vp = (da + 1 == ds + 1) ? hi : vp;
-        }
-        vm = row_or_u32(vm);
-        vp = row_or_u32(vp);
-        if (ds > 0 && ds < D - 1) {
-            const int a = (int)vm, b = (int)(best >> 16), c = (int)vp;
-            const int den = a - 2 * b + c;
-            if (den > 0) v = v + (float)(a - c) / (float)(2 * den);
-        }
-    }
+    float v;
+    const int ds = wta_pick<DPL>(S, k, D, dmin, sub != nullptr, &v);
     if (k == 0) {
         disp[pix] = (uint16_t)(dmin + ds);
         if (sub) sub[pix] = v;
@@ -215,14 +164,6 @@ __global__ void lr_check_kernel(uint16_t* __restrict__ dl, const uint16_t* __res
 
 hipError_t launch_wta_from_paths(Ctx& c, const uint8_t* L8, int W, int H, int D, int dmin,
                                  uint16_t* disp, float* sub) {
-#ifdef SVA_PATHS_ABLATION
-    static int once = [] {
-        int v = getenv("SVA_WTA_NT") ? atoi(getenv("SVA_WTA_NT")) : 1;
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wta_nt), &v, sizeof(int));
-        return 0;
-    }();
-    (void)once;
-#endif
     ScopedKernelTimer t(c, "wta");
     const int npix = W * H;
     const size_t vol = (size_t)npix * D;

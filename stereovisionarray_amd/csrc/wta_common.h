@@ -1,0 +1,63 @@
+// wta_common.h -- first-minimum WTA + parabola sub-pixel on one 16-lane DPP
+// row, shared by wta.hip and wta_h.hip.
+//
+// Lane k holds S(d) for d in [k*DPL, k*DPL + DPL) as DPL/2 packed u16 pairs
+// (lo half = even d).  The first minimum is a u32 min over keys (S << 16 | d):
+// the smaller d wins ties, mirroring std::min_element at
+// CameraStereoVision.cpp:85.  S(d*-1), S(d*+1) come from a DPP OR-reduce.
+#pragma once
+
+#include "sva_device.h"
+
+namespace sva {
+
+__device__ __forceinline__ unsigned row_or_u32(unsigned v) {
+    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_QUAD_1032, 0xf, 0xf, false);
+    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_QUAD_2301, 0xf, 0xf, false);
+    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_HALF_MIRROR, 0xf, 0xf, false);
+    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_MIRROR, 0xf, 0xf, false);
+    return v;
+}
+
+// Returns d* (0-based, the same in all 16 lanes of the row) and, when
+// want_sub, the f32 sub-pixel disparity dmin + d* (+ parabola offset) in *v.
+template <int DPL>
+__device__ __forceinline__ int wta_pick(const unsigned (&S)[DPL / 2], int k, int D, int dmin,
+                                        bool want_sub, float* v) {
+    constexpr int NP = DPL / 2;
+    const int d0 = k * DPL;
+    unsigned best = 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+        const unsigned lo = ((S[j] & 0xffffu) << 16) | (unsigned)(d0 + 2 * j);
+        const unsigned hi = (S[j] & 0xffff0000u) | (unsigned)(d0 + 2 * j + 1);
+        best = best < lo ? best : lo;
+        best = best < hi ? best : hi;
+    }
+    best = row_min_u32(best);
+    const int ds = (int)(best & 0xffffu);
+    float r = (float)(dmin + ds);
+    if (want_sub) {
+        unsigned vm = 0, vp = 0;
+#pragma unroll
+        for (int j = 0; j < NP; j++) {
+            const int da = d0 + 2 * j;
+            const unsigned lo = S[j] & 0xffffu, hi = S[j] >> 16;
+            vm = (da == ds - 1) ? lo : vm;
+            vm = (da + 1 == ds - 1) ? hi : vm;
+            vp = (da == ds + 1) ? lo : vp;
+            vp = (da + 1 == ds + 1) ? hi : vp;
+        }
+        vm = row_or_u32(vm);
+        vp = row_or_u32(vp);
+        if (ds > 0 && ds < D - 1) {
+            const int a = (int)vm, b = (int)(best >> 16), c = (int)vp;
+            const int den = a - 2 * b + c;
+            if (den > 0) r = r + (float)(a - c) / (float)(2 * den);
+        }
+    }
+    *v = r;
+    return ds;
+}
+
+}  // namespace sva
