@@ -296,7 +296,8 @@ def breakdown(a, step, world, ctx, timed_kernels):
     return kernels
 
 
-def kernel_table(ctx, names=("census", "cost", "sgm_paths", "sgm_fused", "wta", "fuse_depth")):
+def kernel_table(ctx, names=("census", "cost", "sgm_paths", "sgm_fused", "wta", "wta_h",
+                              "fuse_depth")):
     """Average hipEvent duration per kernel, pooled over one or several contexts
     (with --streams > 1 the launches overlap, so durations include contention)."""
     ctxs = ctx if isinstance(ctx, list) else [ctx]

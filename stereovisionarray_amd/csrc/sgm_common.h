@@ -67,24 +67,24 @@ struct Words {
     unsigned w[NW];
 };
 
-template <int NW>
 // Cache-policy bits of the C loads.  A/B (full frame, in-process): nt (2)
 // +8 %, sc0+nt (3) +8 %; sc0 (1), sc0+sc1 (17), 8, 16 within the +-2 % noise.
 #ifndef SVA_C_LOAD_AUX
 #define SVA_C_LOAD_AUX 0
 #endif
+template <int NW, int AUX = SVA_C_LOAD_AUX>
 __device__ __forceinline__ Words<NW> bload(rsrc_t r, unsigned off) {
     Words<NW> o;
     if constexpr (NW == 1) {
-        o.w[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, SVA_C_LOAD_AUX);
+        o.w[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX);
     } else if constexpr (NW == 2) {
-        auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, SVA_C_LOAD_AUX);
+        auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX);
         o.w[0] = v[0]; o.w[1] = v[1];
     } else if constexpr (NW == 3) {
-        auto v = __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, SVA_C_LOAD_AUX);
+        auto v = __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, AUX);
         o.w[0] = v[0]; o.w[1] = v[1]; o.w[2] = v[2];
     } else {
-        auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, SVA_C_LOAD_AUX);
+        auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
         o.w[0] = v[0]; o.w[1] = v[1]; o.w[2] = v[2]; o.w[3] = v[3];
     }
     return o;

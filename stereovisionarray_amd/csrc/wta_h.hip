@@ -40,8 +40,20 @@ struct WtaHGeom {
 
 // Prefetch depth (steps) of the backward pass, which loads 7 u8 vectors per
 // step; the forward pass loads 1 and runs a deeper ring.
-template <int DPL> constexpr int pf_fwd() { return DPL <= 8 ? 8 : 4; }
-template <int DPL> constexpr int pf_bwd() { return DPL <= 8 ? 4 : 2; }
+#ifndef SVA_WTAH_PF1
+#define SVA_WTAH_PF1 8
+#endif
+#ifndef SVA_WTAH_PF2
+#define SVA_WTAH_PF2 4
+#endif
+template <int DPL> constexpr int pf_fwd() { return DPL <= 8 ? SVA_WTAH_PF1 : SVA_WTAH_PF1 / 2; }
+template <int DPL> constexpr int pf_bwd() { return DPL <= 8 ? SVA_WTAH_PF2 : SVA_WTAH_PF2 / 2; }
+// Cache policy of the six volume loads (their last use): nt keeps the stream
+// from evicting the segment's cost bytes, which the backward pass re-reads
+// from L2 (PMC: with default loads the kernel fetched C twice from HBM).
+#ifndef SVA_WTAH_VOL_AUX
+#define SVA_WTAH_VOL_AUX 2
+#endif
 
 template <int NW>
 __device__ __forceinline__ void unpack_add(const unsigned (&w)[NW], unsigned (&S)[2 * NW]) {
@@ -140,7 +152,7 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
         const unsigned off = base + (unsigned)(x0 + j) * uD;
         rc[slot] = bload<NW>(rC, off);
 #pragma unroll
-        for (int r = 0; r < 6; r++) rv[slot][r] = bload<NW>(rV[r], off);
+        for (int r = 0; r < 6; r++) rv[slot][r] = bload<NW, SVA_WTAH_VOL_AUX>(rV[r], off);
     };
 #pragma unroll
     for (int q = 0; q < PF2; q++) issue(q, K - 1 - q);

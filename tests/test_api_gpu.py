@@ -106,9 +106,10 @@ def test_reserve_timing_and_errors(ctx, sva):
     ctx.disparity_sgm(L, R, sva.default_params(D=128))
     ctx.disparity_sgm(L, R, sva.default_params(D=128))
     ctx.set_timing(False)
-    for name in ("cost", "sgm_paths", "wta"):
+    for name in ("cost", "sgm_paths", "wta_h"):      # the checkpoint-mode frame pipeline
         ms, n = ctx.kernel_time(name)
         assert n == 2 and ms > 0.0, name
+    assert ctx.kernel_time("wta") == (0.0, 0)
     # 1-D steps without the L/R check, D >= 128: census and cost are one kernel ("cost")
     assert ctx.kernel_time("census") == (0.0, 0)
     # the census-fused path kernel has no cost volume and no cost kernel
@@ -147,7 +148,7 @@ def test_reserve_timing_and_errors(ctx, sva):
     ctx.disparity_sgm(L2, R2, sva.default_params(D=256))      # AUTO: fused
     ctx.set_timing(sva.SVA_TIMING_OFF)
     assert ctx.kernel_time("sgm_paths")[1] == 1 and ctx.kernel_time("sgm_fused")[1] == 1
-    for name in ("census", "cost", "wta"):
+    for name in ("census", "cost", "wta", "wta_h"):
         assert ctx.kernel_time(name) == (0.0, 0), name
     with pytest.raises(sva.SvaError) as e:
         ctx.set_timing(3)

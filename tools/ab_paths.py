@@ -26,7 +26,9 @@ def main():
     ap.add_argument("--H", type=int, default=1080)
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--iters", type=int, default=30)
-    ap.add_argument("--entry", default="paths", choices=["paths", "sgm", "cost", "fused", "census", "census_cost"])
+    ap.add_argument("--entry", default="paths",
+                    choices=["paths", "sgm", "cost", "fused", "census", "census_cost", "ckpt",
+                             "wta_h"])
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -42,6 +44,8 @@ def main():
     disp = torch.zeros((H, W), dtype=torch.int16, device=dev)
     C = torch.zeros((H, W, D), dtype=torch.uint8, device=dev)
     L8 = torch.zeros((8, H, W, D), dtype=torch.uint8, device=dev)
+    ns, _ = sva.ckpt_segments(W, D)
+    CK = torch.zeros((2, H, ns, D), dtype=torch.uint8, device=dev)
     p = sva.default_params(D=D)
     handles = []
     for path in a.libs:
@@ -63,6 +67,9 @@ def main():
     lib0.sva_census_d(h0, ct.c_void_p(dR.data_ptr()), W, H, ct.c_size_t(W), ct.c_void_p(cr.data_ptr()))
     lib0.sva_cost_d(h0, ct.c_void_p(cl.data_ptr()), ct.c_void_p(cr.data_ptr()), W, H, ct.byref(p),
                     ct.c_void_p(C_src.data_ptr()))
+    # checkpoint-mode volumes for the wta_h entry (first library)
+    lib0.sva_paths_ckpt_d(h0, ct.c_void_p(C_src.data_ptr()), W, H, ct.byref(p),
+                          ct.c_void_p(L8.data_ptr()), ct.c_void_p(CK.data_ptr()))
     torch.cuda.synchronize()
     times = {n: [] for n, _, _ in handles}
     ref = None
@@ -73,6 +80,13 @@ def main():
             if a.entry == "paths":
                 st = lib.sva_paths_d(h, ct.c_void_p(C.data_ptr()), W, H, ct.byref(p),
                                      ct.c_void_p(L8.data_ptr()))
+            elif a.entry == "ckpt":
+                st = lib.sva_paths_ckpt_d(h, ct.c_void_p(C.data_ptr()), W, H, ct.byref(p),
+                                          ct.c_void_p(L8.data_ptr()), ct.c_void_p(CK.data_ptr()))
+            elif a.entry == "wta_h":
+                st = lib.sva_wta_h_d(h, ct.c_void_p(C.data_ptr()), ct.c_void_p(L8.data_ptr()),
+                                     ct.c_void_p(CK.data_ptr()), W, H, ct.byref(p),
+                                     ct.c_void_p(disp.data_ptr()), None)
             elif a.entry == "census":
                 st = lib.sva_census_d(h, ct.c_void_p(dL.data_ptr()), W, H, ct.c_size_t(W),
                                       ct.c_void_p(cl.data_ptr()))
@@ -116,6 +130,21 @@ def main():
                 outs.append(torch.sum(L8.view(torch.int64)).item())
             if not os.environ.get("AB_NOCHECK"):
                 assert len(set(outs)) == 1, outs
+        if a.entry in ("ckpt", "wta_h") and it == 0:
+            outs = []
+            for n, lib, h in handles:
+                if a.entry == "ckpt":
+                    lib.sva_paths_ckpt_d(h, ct.c_void_p(C.data_ptr()), W, H, ct.byref(p),
+                                         ct.c_void_p(L8.data_ptr()), ct.c_void_p(CK.data_ptr()))
+                else:
+                    lib.sva_wta_h_d(h, ct.c_void_p(C.data_ptr()), ct.c_void_p(L8.data_ptr()),
+                                    ct.c_void_p(CK.data_ptr()), W, H, ct.byref(p),
+                                    ct.c_void_p(disp.data_ptr()), None)
+                torch.cuda.synchronize()
+                t = L8 if a.entry == "ckpt" else disp
+                outs.append(torch.sum(t.view(torch.int64) if t.dtype == torch.uint8 else
+                                      t.to(torch.int64)).item())
+            assert len(set(outs)) == 1, outs
         if a.entry == "paths" and it == 0:
             # every variant must produce the same volumes
             outs = []

@@ -3,10 +3,12 @@
 MI355X_MICROARCH.md's HBM section prescribes) into per-launch HBM bytes.
 
 gfx950 correction: FETCH_SIZE reports 1/2 of the bytes of a wide coalesced
-stream.  We calibrate instead of assuming: wta_paths_kernel reads exactly the
-8 path volumes (8*W*H*D bytes, each byte once, dwordx2-wide like sgm_paths),
-so fetch_scale = known_bytes / (FETCH_SIZE*1024) for that kernel.  WRITE_SIZE
-is exact for these store widths (sgm_paths writes 8*W*H*D bytes).
+stream.  When the run has wta_paths_kernel (the 8-volume route) we calibrate
+on it instead of assuming: it reads exactly the 8 path volumes (8*W*H*D bytes,
+each byte once, dwordx2-wide like sgm_paths), so fetch_scale = known_bytes /
+(FETCH_SIZE*1024); otherwise the guide's factor 2.0 applies (calibrated on
+wta_paths_kernel at 2.0 in round 1).  WRITE_SIZE is exact for these store
+widths.
 
 usage: pmc_traffic.py FETCH_DIR WRITE_DIR W H D OUT.json
 """
@@ -21,7 +23,7 @@ SHORT = {
     "wta_paths_kernel": "wta", "hamming_cost_kernel": "cost", "census9x7_kernel": "census",
     "hamming_cost2_kernel": "cost2", "fuse_depth_kernel": "fuse_depth",
     "hamming_cost_rows_kernel": "cost", "census9x7_rows_kernel": "census",
-    "census_cost_kernel": "cost",
+    "census_cost_kernel": "cost", "wta_h_kernel": "wta_h",
 }
 
 
