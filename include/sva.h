@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SVA_ABI_VERSION 2
+#define SVA_ABI_VERSION 3
 
 enum {
     SVA_OK = 0,
@@ -307,9 +307,78 @@ int sva_disparity_to_depth(void* ctx, const uint8_t* disp, int n, double cam_dis
 /* -------------------------------------------------- multi-pair batch --- */
 /* Independent pairs round-robin over the given contexts (one per device),
  * one host thread per context.  Replaces the `for (auto pair : pairs)` loop
- * (CameraStereoVision.cpp:55) for whole-image Mode S matching. */
+ * (CameraStereoVision.cpp:55) for whole-image Mode S matching on HOST images.
+ * Per context, the upload of pair j+1 and the download of pair j-1 overlap
+ * the compute of pair j (pinned staging, separate copy streams).  A failing
+ * pair does not stop the others: job_status (nullable, n_jobs entries)
+ * receives each pair's status and the call returns the first failure. */
 int sva_batch_sgm(void** ctxs, int n_ctx, const sva_pair_job* jobs, int n_jobs,
-                  const sva_sgm_params* p);
+                  const sva_sgm_params* p, int* job_status);
+
+/* ----------------------------------- multi-GPU engine --- */
+/* One process drives several GPUs of a node: pairs are the shard unit (pair j
+ * -> device j mod n_devices, and round-robin over that device's streams), each
+ * device keeps its own cost and path volumes, and the only exchange is the
+ * gather of the finished u16 disparity maps (and f32 sub-pixel maps) to
+ * devices[0] over xGMI -- an RCCL grouped send/recv on a single-process
+ * communicator (ncclCommInitAll, librccl loaded at sva_multi_create), or peer
+ * copies with SVA_MULTI_GATHER_PEER.  north_star / BASELINE configs 4-5;
+ * replaces the pair loop at CameraStereoVision.cpp:55 with the pair tables of
+ * functions.cpp:148-213 (sva.hpp getCameraPairs). */
+#define SVA_MULTI_GATHER_RCCL 0   /* default */
+#define SVA_MULTI_GATHER_PEER 1
+#define SVA_MULTI_GATHER_ALL 2    /* flag: route device 0's own maps through the
+                                     gather too (exercises the exchange on one GPU) */
+int sva_multi_create(const int* devices, int n_devices, int streams_per_device, int flags,
+                     void** multi_out);
+int sva_multi_destroy(void* multi);
+/* Block until every queued batch has finished on every device. */
+int sva_multi_synchronize(void* multi);
+const char* sva_multi_last_error(void* multi);
+/* The shard plan, a pure function (no device needed): for job j,
+ * device_index[j] = j mod n_devices and context_index[j] = (j / n_devices) mod
+ * streams_per_device (nullable outputs); slot_index[j] = rank of j among the
+ * jobs of its context (nullable). */
+int sva_multi_plan(int n_devices, int streams_per_device, int n_jobs, int32_t* device_index,
+                   int32_t* context_index, int32_t* slot_index);
+/* The context behind (device_index, stream_index), e.g. for sva_set_timing. */
+int sva_multi_context(void* multi, int device_index, int stream_index, void** ctx_out);
+
+/* One device-resident pair: left/right live on device
+ * devices[j mod n_devices] (see sva_multi_plan), pitch in bytes. */
+typedef struct sva_pair_d {
+    const uint8_t* left;
+    const uint8_t* right;
+    sva_sgm_params params;
+} sva_pair_d;
+/* Every pair's Mode S map, gathered into maps (device memory on devices[0],
+ * [n_jobs][H][W] u16) and, when subpix is non-NULL and params.subpixel is
+ * set, the f32 maps into subpix ([n_jobs][H][W] on devices[0]).  Asynchronous:
+ * the results are complete on devices[0]'s first stream (stream_index 0)
+ * once the call returns SVA_OK and that stream has run; sva_multi_synchronize
+ * waits for everything. */
+int sva_batch_sgm_d(void* multi, const sva_pair_d* jobs, int n_jobs, int width, int height,
+                    size_t pitch, uint16_t* maps, float* subpix);
+
+/* A camera-array frame from HOST images: pair j matches images[pairs[j].ref]
+ * against images[pairs[j].other] with its own params (the 2-D step of its
+ * baseline) on device j mod n_devices; the maps are gathered to devices[0],
+ * which fuses group g = pairs [group_start[g], group_start[g+1]) (one
+ * reference camera, DESIGN.md §2.6, with pairs[j].baseline) into depth[g].
+ * Uploads run on per-device copy streams and each pair waits only for its two
+ * images, so transfers overlap compute; the fused maps download as each group
+ * finishes.  depth: host [n_groups][H][W] f64; n_valid (nullable) host u8,
+ * same shape; maps (nullable) host [n_pairs][H][W] u16.  Synchronous. */
+typedef struct sva_array_pair {
+    int32_t ref;              /* index into images[]: the reference view      */
+    int32_t other;            /* index into images[]: the matched view        */
+    sva_sgm_params params;    /* D, dmin, (dir, dir_y) = this pair's step     */
+    double baseline;          /* major-axis baseline (m) for the fusion       */
+} sva_array_pair;
+int sva_array_depth(void* multi, const uint8_t* const* images, int n_images, int width,
+                    int height, size_t pitch, const sva_array_pair* pairs, int n_pairs,
+                    const int32_t* group_start, int n_groups, double f, double pixel_size,
+                    double* depth, uint8_t* n_valid, uint16_t* maps);
 
 #ifdef __cplusplus
 }

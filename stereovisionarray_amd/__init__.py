@@ -49,8 +49,13 @@ EXPORTED = [
     "sva_depth_to_points", "sva_resize_half_size", "sva_resize_half_d", "sva_resize_half",
     "sva_batch_sgm", "sva_resize_linear_f64_d", "sva_resize_linear_f64", "sva_ref_error_d",
     "sva_ref_error", "sva_masked_mean_d", "sva_masked_mean", "sva_ckpt_segments",
-    "sva_paths_ckpt_d", "sva_wta_h_d",
+    "sva_paths_ckpt_d", "sva_wta_h_d", "sva_multi_create", "sva_multi_destroy",
+    "sva_multi_synchronize", "sva_multi_last_error", "sva_multi_plan", "sva_multi_context",
+    "sva_batch_sgm_d", "sva_array_depth",
 ]
+SVA_MULTI_GATHER_RCCL = 0
+SVA_MULTI_GATHER_PEER = 1
+SVA_MULTI_GATHER_ALL = 2
 
 
 class SgmParams(ct.Structure):
@@ -82,6 +87,17 @@ class PairJob(ct.Structure):
         ("height", ct.c_int32), ("pitch", ct.c_size_t), ("disp", ct.c_void_p),
         ("subpix", ct.c_void_p),
     ]
+
+
+class PairD(ct.Structure):
+    """sva_pair_d: one device-resident pair for sva_batch_sgm_d."""
+    _fields_ = [("left", ct.c_void_p), ("right", ct.c_void_p), ("params", SgmParams)]
+
+
+class ArrayPair(ct.Structure):
+    """sva_array_pair: one camera-array pair for sva_array_depth."""
+    _fields_ = [("ref", ct.c_int32), ("other", ct.c_int32), ("params", SgmParams),
+                ("baseline", ct.c_double)]
 
 
 class SvaError(RuntimeError):
@@ -165,7 +181,16 @@ def _load() -> ct.CDLL:
         "sva_resize_half_size": (i32, [i32, i32, P(i32), P(i32)]),
         "sva_resize_half_d": (i32, [vp, vp, i32, i32, sz, vp, sz]),
         "sva_resize_half": (i32, [vp, vp, i32, i32, sz, vp, sz]),
-        "sva_batch_sgm": (i32, [P(vp), i32, P(PairJob), i32, P(SgmParams)]),
+        "sva_batch_sgm": (i32, [P(vp), i32, P(PairJob), i32, P(SgmParams), P(i32)]),
+        "sva_multi_create": (i32, [P(i32), i32, i32, i32, P(vp)]),
+        "sva_multi_destroy": (i32, [vp]),
+        "sva_multi_synchronize": (i32, [vp]),
+        "sva_multi_last_error": (ct.c_char_p, [vp]),
+        "sva_multi_plan": (i32, [i32, i32, i32, P(i32), P(i32), P(i32)]),
+        "sva_multi_context": (i32, [vp, i32, i32, P(vp)]),
+        "sva_batch_sgm_d": (i32, [vp, P(PairD), i32, i32, i32, sz, vp, vp]),
+        "sva_array_depth": (i32, [vp, P(vp), i32, i32, i32, sz, P(ArrayPair), i32, P(i32), i32,
+                                  dbl, dbl, vp, vp, vp]),
         "sva_resize_linear_f64_d": (i32, [vp, vp, i32, i32, vp, i32, i32]),
         "sva_resize_linear_f64": (i32, [vp, vp, i32, i32, vp, i32, i32]),
         "sva_ref_error_d": (i32, [vp, vp, i32, i32, vp, i32, i32, ct.c_double, vp]),
@@ -508,8 +533,10 @@ class Context:
 
 
 def batch_sgm(contexts: list[Context], pairs: list[tuple[np.ndarray, np.ndarray]],
-              params: SgmParams):
-    """Match independent pairs round-robin over ``contexts`` (``sva_batch_sgm``)."""
+              params: SgmParams, statuses: list | None = None):
+    """Match independent pairs round-robin over ``contexts`` (``sva_batch_sgm``).
+    With ``statuses`` (a list), per-pair status codes are appended to it and a
+    failing pair does not raise; otherwise the first failure raises."""
     jobs = (PairJob * len(pairs))()
     outs = []
     keep = []
@@ -523,7 +550,88 @@ def batch_sgm(contexts: list[Context], pairs: list[tuple[np.ndarray, np.ndarray]
         outs.append((d, s))
         jobs[i] = PairJob(_ptr(l), _ptr(r), W, H, W, _ptr(d), _ptr(s))
     hs = (ct.c_void_p * len(contexts))(*[c.h.value for c in contexts])
-    st = lib.sva_batch_sgm(hs, len(contexts), jobs, len(pairs), ct.byref(params))
-    if st != SVA_OK:
+    js = (ct.c_int * max(1, len(pairs)))()
+    st = lib.sva_batch_sgm(hs, len(contexts), jobs, len(pairs), ct.byref(params), js)
+    if statuses is not None:
+        statuses.extend(js[:len(pairs)])
+    elif st != SVA_OK:
         raise SvaError(st, lib.sva_status_string(st).decode())
     return outs
+
+
+def multi_plan(n_devices: int, streams: int, n_jobs: int):
+    """(device_index, context_index, slot_index) arrays of sva_multi_plan."""
+    d = np.zeros(max(n_jobs, 1), np.int32)
+    c = np.zeros(max(n_jobs, 1), np.int32)
+    s = np.zeros(max(n_jobs, 1), np.int32)
+    st = lib.sva_multi_plan(n_devices, streams, n_jobs,
+                            d.ctypes.data_as(ct.POINTER(ct.c_int32)),
+                            c.ctypes.data_as(ct.POINTER(ct.c_int32)),
+                            s.ctypes.data_as(ct.POINTER(ct.c_int32)))
+    if st != SVA_OK:
+        raise SvaError(st, "sva_multi_plan")
+    return d[:n_jobs], c[:n_jobs], s[:n_jobs]
+
+
+class Multi:
+    """The multi-GPU engine (sva_multi_*): pairs shard over ``devices`` (pair j
+    -> device j mod N, round-robin over ``streams`` contexts per device) and
+    the maps are gathered to devices[0] (RCCL or peer copies)."""
+
+    def __init__(self, devices, streams: int = 2, flags: int = SVA_MULTI_GATHER_RCCL):
+        self.devices = list(devices)
+        arr = (ct.c_int * len(self.devices))(*self.devices)
+        self.h = ct.c_void_p()
+        st = lib.sva_multi_create(arr, len(self.devices), streams, flags, ct.byref(self.h))
+        if st != SVA_OK:
+            raise SvaError(st, f"sva_multi_create ({lib.sva_status_string(st).decode()})")
+
+    def close(self):
+        if self.h:
+            lib.sva_multi_destroy(self.h)
+            self.h = ct.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, st: int):
+        if st != SVA_OK:
+            raise SvaError(st, lib.sva_multi_last_error(self.h).decode(errors="replace"))
+
+    def synchronize(self):
+        self._chk(lib.sva_multi_synchronize(self.h))
+
+    def context_handle(self, device_index: int, stream_index: int) -> int:
+        out = ct.c_void_p()
+        self._chk(lib.sva_multi_context(self.h, device_index, stream_index, ct.byref(out)))
+        return out.value
+
+    def batch_sgm_d(self, pairs, W, H, pitch, maps, sub=None):
+        """pairs: list of (left_ptr, right_ptr, SgmParams) on their owner devices."""
+        jobs = (PairD * len(pairs))()
+        for i, (l, r, p) in enumerate(pairs):
+            jobs[i] = PairD(_ptr(l), _ptr(r), p)
+        self._chk(lib.sva_batch_sgm_d(self.h, jobs, len(pairs), W, H, pitch, _ptr(maps),
+                                      _ptr(sub)))
+
+    def array_depth(self, images, pairs, group_start, f, pixel_size, want_maps=False):
+        """images: list of HxW u8 numpy views; pairs: list of (ref, other,
+        SgmParams, baseline); group_start: n_groups + 1 offsets.  Returns
+        (depth [G,H,W] f64, n_valid [G,H,W] u8, maps [P,H,W] u16 or None)."""
+        imgs = [np.ascontiguousarray(a, dtype=np.uint8) for a in images]
+        H, W = imgs[0].shape
+        ptrs = (ct.c_void_p * len(imgs))(*[_ptr(a) for a in imgs])
+        jp = (ArrayPair * len(pairs))()
+        for i, (a, b, p, base) in enumerate(pairs):
+            jp[i] = ArrayPair(a, b, p, base)
+        gs = (ct.c_int32 * len(group_start))(*group_start)
+        G = len(group_start) - 1
+        depth = np.zeros((G, H, W), np.float64)
+        nv = np.zeros((G, H, W), np.uint8)
+        maps = np.zeros((len(pairs), H, W), np.uint16) if want_maps else None
+        self._chk(lib.sva_array_depth(self.h, ptrs, len(imgs), W, H, W, jp, len(pairs), gs, G,
+                                      f, pixel_size, _ptr(depth), _ptr(nv), _ptr(maps)))
+        return depth, nv, maps

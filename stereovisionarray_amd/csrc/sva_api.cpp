@@ -1199,32 +1199,4 @@ int sva_masked_mean(void* ctx, const double* image, const uint8_t* mask, int w, 
                              h, mean);
 }
 
-// ---------------------------------------------------------------- batch --
-int sva_batch_sgm(void** ctxs, int n_ctx, const sva_pair_job* jobs, int n_jobs,
-                  const sva_sgm_params* p) {
-    if (!ctxs || n_ctx <= 0 || (n_jobs > 0 && !jobs) || n_jobs < 0 || !p)
-        return SVA_ERR_INVALID_ARG;
-    for (int i = 0; i < n_ctx; i++)
-        if (!ctxs[i]) return SVA_ERR_INVALID_ARG;
-    std::vector<int> status(n_ctx, SVA_OK);
-    std::vector<std::thread> th;
-    for (int i = 0; i < n_ctx; i++) {
-        th.emplace_back([&, i]() {
-            for (int j = i; j < n_jobs; j += n_ctx) {  // pair j -> context j mod N
-                const sva_pair_job& J = jobs[j];
-                int s = sva_disparity_sgm(ctxs[i], J.left, J.right, J.width, J.height, J.pitch, p,
-                                          J.disp, J.subpix);
-                if (s != SVA_OK) {
-                    status[i] = s;
-                    return;
-                }
-            }
-        });
-    }
-    for (auto& t : th) t.join();
-    for (int s : status)
-        if (s != SVA_OK) return s;
-    return SVA_OK;
-}
-
 }  // extern "C"
