@@ -296,6 +296,60 @@ def breakdown(a, step, world, ctx, timed_kernels):
     return kernels
 
 
+def exchange_report(a, step, world, rank, dev, ctxs, last, n_units, ms_per_step, recompute):
+    """The path's one exchange, checked and timed once after the timed region
+    (N > 1, or the 1-rank RCCL rehearsal):
+      * the last step's maps are gathered again with a per-unit checksum that
+        each owner computed before sending (dist.gather_maps_checked), and
+        rank 0 checks every received map against it;
+      * rank 0 recomputes one unit owned by another rank (unit 1, or unit 0
+        at N = 1) from its seed and compares the bytes with the gathered map;
+      * the gather alone is timed, and the steps are re-timed without it: the
+        difference is the gather time the overlap does not hide.
+    Returns the report on rank 0 (None elsewhere)."""
+    import torch
+    import torch.distributed as dist
+    from stereovisionarray_amd import dist as sdist
+    gloo = a.dist_backend == "gloo" and world > 1
+    torch.cuda.synchronize()
+    src = last.cpu() if gloo else last
+    maps, ok = sdist.gather_maps_checked(src, n_units, dst=0)
+    remote = None
+    if rank == 0:
+        u = 1 if n_units > 1 else 0
+        mine = recompute(u)
+        torch.cuda.synchronize()
+        remote = {"unit": u, "owner_rank": u % world,
+                  "equal": bool(torch.equal(mine.cpu(), maps[u].cpu()))}
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cpu" if gloo else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    n = min(a.steps, 10)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        sdist.gather_maps(src, n_units, dst=0)
+    torch.cuda.synchronize()
+    gather_ms = max_over_ranks((time.perf_counter() - t0) / n * 1e3)
+    compute_ms = timed(a, lambda: step(False), world, dev, ctxs) / a.steps * 1e3
+    if rank != 0:
+        return None
+    return {"backend": "gloo" if gloo else "rccl", "world": dist.get_world_size(),
+            "rccl_world": None if gloo else dist.get_world_size(),
+            "units_checked": n_units, "checksums_ok": ok, "remote_unit_recomputed": remote,
+            "ok": bool(ok and remote["equal"]),
+            "gather_ms": round(gather_ms, 4),
+            "compute_only_ms_per_step": round(compute_ms, 4),
+            "exposed_gather_ms_per_step": round(ms_per_step - compute_ms, 4),
+            "map_bytes_per_unit": int(last[0].numel() * last.element_size())}
+
+
 def kernel_table(ctx, names=("census", "cost", "sgm_paths", "sgm_fused", "wta", "wta_h",
                               "fuse_depth")):
     """Average hipEvent duration per kernel, pooled over one or several contexts
@@ -341,6 +395,19 @@ def roofline_of(kernels, W, H, D, workload, overlapped=False):
         # other stream's kernels, so this fraction is not the single-stream one
         out["overlapped"] = True
     return out
+
+
+def frame_roofline(W, H, D, ms_per_frame):
+    """The whole frame against SURVEY §8d's per-stage algorithmic bytes:
+    census 18 B/px, cost 16 B/px + 1 B/disp, aggregation 10 B/disp, WTA
+    2 B/disp + 2 B/px, over the measured time per frame (all kernels and the
+    launch gaps between them)."""
+    alg = 13.0 * W * H * D + 36.0 * W * H
+    ach = alg / (ms_per_frame * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_frame": alg,
+            "ms_per_frame": round(ms_per_frame, 4),
+            "model": "SURVEY §8d census+cost+aggregation+WTA: 13 B/disp + 36 B/px"}
 
 
 def rig_of(name):
@@ -414,7 +481,11 @@ def run_array(a, wl, world, rank, local, dev):
         ctxs.append(c_)
         cstreams.append(s_)
 
-    def step():
+    # compute-only steps (exchange_report) fuse a stand-in buffer of the full size
+    stand_in = torch.zeros((n_units, H, W), dtype=torch.int16, device=dev) \
+        if world > 1 and rank == 0 else None
+
+    def step(exchange=True):
         if len(ctxs) > 1:                # the previous step's fusion has read disp
             go = torch.cuda.Event()
             go.record(stream)
@@ -427,7 +498,9 @@ def run_array(a, wl, world, rank, local, dev):
             done_ = torch.cuda.Event()
             done_.record(s_)
             stream.wait_event(done_)
-        if world > 1:
+        if world > 1 and not exchange:
+            allm = stand_in
+        elif world > 1:
             if a.dist_backend == "nccl":
                 allm = sdist.gather_maps(disp, n_units, dst=0)
             else:
@@ -444,6 +517,21 @@ def run_array(a, wl, world, rank, local, dev):
     elapsed = timed(a, step, world, dev, ctxs)
     kernels = breakdown(a, step, world, ctxs, kernel_table(ctxs))
     value = n_units * W * H * D * a.steps / elapsed / 1e6
+    exchange = None
+    if world > 1:
+        def recompute(u):
+            i, j = pairs[u]
+            sx, sy, _ = synth.pair_step(grid[i], grid[j])
+            Ld = torch.from_numpy(views_np[i]).to(dev)
+            Rd = torch.from_numpy(views_np[j]).to(dev)
+            m = torch.zeros((H, W), dtype=torch.int16, device=dev)
+            ctx.disparity_sgm_d(Ld.data_ptr(), Rd.data_ptr(), W, H, W,
+                                sva.default_params(D=D, dmin=0, dir=sx, dir_y=sy), m.data_ptr())
+            return m
+        exchange = exchange_report(a, step, world, rank, dev, ctxs, disp, n_units,
+                                   elapsed / a.steps * 1e3, recompute)
+        step()                           # the compute-only steps fused the stand-in
+        torch.cuda.synchronize()
     out = None
     if rank == 0:
         # sanity: camera 0 sees the texture unwarped, so its fused depth must be
@@ -485,6 +573,8 @@ def run_array(a, wl, world, rank, local, dev):
             "roofline": roofline_of(kernels, W, H, D, "1080p_d128", overlapped=len(ctxs) > 1),
             "cpu_baseline": None,
         }
+        if exchange is not None:
+            out["exchange"] = exchange
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(W, H, D, a.cpu_threads)
         print(json.dumps(out), flush=True)
@@ -492,6 +582,8 @@ def run_array(a, wl, world, rank, local, dev):
         c.close()
     if world > 1:
         dist.destroy_process_group()
+    if exchange is not None and not exchange["ok"]:
+        raise SystemExit("multi-rank exchange check failed: " + json.dumps(exchange))
 
 
 def main():
@@ -587,12 +679,13 @@ def main():
         else:                            # --rehearse-overlap stand-in for the RCCL gather
             rehearsal[0].copy_(disp)
 
-    def step():
+    def step(exchange=True):
         b = it[0] % nbuf
         it[0] += 1
         disp = disps[b]
         if gathered[b] is not None:      # the previous gather of this buffer is done
             stream.wait_event(gathered[b])
+            gathered[b] = None
         if len(ctxs) > 1:                # other streams start after this buffer is free
             go = torch.cuda.Event()
             go.record(stream)
@@ -605,7 +698,7 @@ def main():
             done_ = torch.cuda.Event()
             done_.record(s_)
             stream.wait_event(done_)
-        if world > 1 or comm is not None:   # the path's one exchange: maps -> rank 0 (RCCL)
+        if exchange and (world > 1 or comm is not None):   # the path's one exchange (RCCL)
             if a.dist_backend == "gloo" and world > 1:
                 sdist.gather_maps(disp.cpu(), n_units, dst=0)
             elif comm is None:
@@ -629,6 +722,16 @@ def main():
         last = disps[(it[0] - 1) % nbuf]
         assert torch.equal(rehearsal[0], last), "overlapped gather copied the wrong buffer"
     assert d0.max() < D, "disparity out of range"
+    exchange = None
+    if world > 1 or rccl1:
+        def recompute(u):
+            L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=seed0 + u)
+            Ld, Rd = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
+            m = torch.zeros((H, W), dtype=torch.int16, device=dev)
+            ctx.disparity_sgm_d(Ld.data_ptr(), Rd.data_ptr(), W, H, W, params, m.data_ptr())
+            return m
+        exchange = exchange_report(a, step, world, rank, dev, ctxs, disps[(it[0] - 1) % nbuf],
+                                   n_units, elapsed / a.steps * 1e3, recompute)
 
     units = world * P * a.steps
     disparities = units * W * H * D
@@ -661,6 +764,10 @@ def main():
         "roofline": roofline,
         "cpu_baseline": None,
     }
+    if len(ctxs) == 1:
+        out["frame_roofline"] = frame_roofline(W, H, D, ms_per_step / P)
+    if exchange is not None:
+        out["exchange"] = exchange
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(W, H, D, a.cpu_threads)
         _, _, budget = host_cpu()
@@ -676,6 +783,8 @@ def main():
         c.close()
     if world > 1 or rccl1:
         dist.destroy_process_group()
+    if exchange is not None and not exchange["ok"]:
+        raise SystemExit("multi-rank exchange check failed: " + json.dumps(exchange))
 
 
 if __name__ == "__main__":

@@ -62,3 +62,41 @@ def gather_maps(local: torch.Tensor, n_units: int, dst: int = 0,
         return out.view(dtype).reshape((n_units,) + shape)
     dist.gather(send.contiguous(), None, dst=dst, group=group)
     return None
+
+
+def _row_bytes(t: torch.Tensor) -> int:
+    row = t.element_size()
+    for n in t.shape[1:]:
+        row *= n
+    return row
+
+
+def checksums(maps: torch.Tensor) -> torch.Tensor:
+    """Per-unit checksum of maps [n, ...] as int64 [n]: a position-weighted
+    byte sum (weights 1..251 repeating), so swapped units, shifted rows and
+    single-byte errors all change it.  Runs on the maps' device."""
+    n, row = maps.shape[0], _row_bytes(maps)
+    b = maps.contiguous().view(torch.uint8).reshape(n, row).to(torch.int64)
+    w = torch.arange(b.shape[1], device=b.device, dtype=torch.int64) % 251 + 1
+    return (b * w).sum(1)
+
+
+def gather_maps_checked(local: torch.Tensor, n_units: int, dst: int = 0, group=None):
+    """gather_maps with a per-unit checksum computed by the owning rank and
+    shipped with its map: on `dst` returns (maps [n_units, ...], ok) where ok
+    says every received map matches the checksum its owner computed before
+    sending; (None, True) elsewhere.  Used once per run by bench.py to check
+    the multi-rank exchange (the timed steps use plain gather_maps)."""
+    n = local.shape[0]
+    row = local.contiguous().view(torch.uint8).reshape(n, _row_bytes(local))
+    ck = checksums(local).view(torch.uint8).reshape(n, 8)
+    packed = torch.cat([row, ck], 1)
+    out = gather_maps(packed, n_units, dst=dst, group=group)
+    if out is None:
+        return None, True
+    maps = out[:, :-8].contiguous()
+    sent = out[:, -8:].contiguous().view(torch.int64).reshape(n_units)
+    shape = (n_units,) + tuple(local.shape[1:])
+    maps = maps.view(local.dtype).reshape(shape)
+    ok = bool(torch.equal(checksums(maps), sent))
+    return maps, ok

@@ -35,11 +35,12 @@ def _worker(rank, world, port, n_units, q):
         local = torch.stack([fake_map(u) for u in mine]) if mine else torch.zeros((0, 6, 10),
                                                                                   dtype=torch.int16)
         out = sdist.gather_maps(local, n_units)
+        chk, ok = sdist.gather_maps_checked(local, n_units)
         if rank == 0:
             exp = torch.stack([fake_map(u) for u in range(n_units)])
-            q.put(("ok", bool(torch.equal(out, exp))))
+            q.put(("ok", bool(torch.equal(out, exp)) and bool(torch.equal(chk, exp)) and ok))
         else:
-            q.put(("ok", out is None))
+            q.put(("ok", out is None and chk is None and ok))
     except Exception as e:  # pragma: no cover - surfaced through the queue
         q.put(("err", repr(e)))
     finally:
@@ -58,6 +59,20 @@ def test_gather_matches_single_rank(world, n_units):
     for p in procs:
         p.join(timeout=60)
     assert all(r == ("ok", True) for r in res), res
+
+
+def test_checksums_detect_swaps_and_byte_errors():
+    maps = torch.stack([fake_map(u) for u in range(4)])
+    base = sdist.checksums(maps)
+    assert len(set(base.tolist())) == 4
+    swapped = maps[[1, 0, 2, 3]]
+    assert not torch.equal(sdist.checksums(swapped), base)
+    flipped = maps.clone()
+    flipped[2, 3, 4] ^= 1
+    got = sdist.checksums(flipped)
+    assert got[2] != base[2] and torch.equal(got[[0, 1, 3]], base[[0, 1, 3]])
+    rolled = torch.roll(maps, 1, dims=2)          # a shifted row layout
+    assert not torch.equal(sdist.checksums(rolled), base)
 
 
 def test_shard_covers_every_unit_once():
