@@ -193,27 +193,19 @@ __global__ __launch_bounds__(256) void ref_match_kernel(
 //
 // For a fixed offset delta, AD(q) = |O(q + delta) - R(q)| is shared by every
 // reference pixel, and SAD(p, delta) is the 2k x 2k box sum of AD at p.  A
-// workgroup owns a tile of TW = 64 - 2k columns x PT_ROWS rows of reference
-// pixels, whose window-extended region is exactly 64 columns wide.  It
+// workgroup owns a tile of reference pixels and
 //   1. collects the union of its pixels' candidate offsets c_i - p in an LDS
 //      bitmap over their bounding box (neighbouring pixels' offsets nearly
 //      coincide, so this is a thin band even for diagonal pairs);
-//   2. per offset plane: AD bytes of the region into LDS (aligned dword loads
-//      of O realigned with v_alignbyte), column sums sliding down the rows,
-//      row sums sliding along x, and for each pixel a division-free test of
-//      whether delta is on ITS Bresenham line -- candidate i on a low line is
-//      x0 + i with minor offset m = floor((a*i + major - 1) / b), i.e.
-//      t*b <= a*i + major - 1 < (t+1)*b for t = step*(c.minor - minor0) --
-//      keeping min over (SAD << 32 | i): the reference's first minimum
-//      (CameraStereoVision.cpp:85) whatever order the planes are visited in.
+//   2. per offset plane forms the box sums of the tile and, for each pixel,
+//      tests whether delta is on ITS Bresenham line -- candidate i has minor
+//      offset floor((a*i + major - 1) / b) -- keeping the minimum key over
+//      (SAD, i): the reference's first minimum (CameraStereoVision.cpp:85)
+//      whatever order the planes are visited in.
 // A tile whose offset box exceeds the bitmap falls back to match_pixel_wave.
-constexpr int PT_ROWS = 32;                  // tile rows
-constexpr int PT_REG_W = 64;                 // region width = TW + 2k
-constexpr int PT_MAXK = 28;                  // TW >= 8
-constexpr int PT_REG_H = PT_ROWS + 2 * PT_MAXK;
-constexpr int PT_P_W = PT_REG_W + 1;         // prefix rows: 65 u32 (odd stride spreads banks)
+constexpr int PT_REG_W = 64;                 // v2 region width = TW + 2k
+constexpr int PT_MAXK = 28;                  // largest k of the plane kernels
 constexpr int PT_MAXBITS = 1 << 15;          // offset bitmap capacity
-constexpr int PT_OU_BYTES = 28 * 1024;       // staged union of O over all planes (3 workgroups/CU)
 
 // Inclusive wave64 scan in 6 DPP adds (no LDS): Hillis-Steele within each
 // 16-lane row (row_shr 1, 2, 4, 8; lanes with no source read 0), then
@@ -230,215 +222,15 @@ __device__ __forceinline__ unsigned scan64_dpp(unsigned v) {
     return v;
 }
 
-__device__ __forceinline__ bool on_line(const Line& L, int cx, int cy) {
-    int i, t;
-    if (L.high) { i = cy - L.y0; t = L.step * (cx - L.x0); }
-    else { i = cx - L.x0; t = L.step * (cy - L.y0); }
-    if (i < 0 || i >= L.n) return false;
-    if (L.b == 0) return t == 0;
-    const int num = L.a * i + L.major - 1;
-    return t >= 0 && t * L.b <= num && num < (t + 1) * L.b;
-}
-
-__device__ __forceinline__ int line_index(const Line& L, int cx, int cy) {
-    return L.high ? cy - L.y0 : cx - L.x0;
-}
-
-template <int ND>
-__global__ __launch_bounds__(256) void ref_plane_kernel(
-    const uint8_t* __restrict__ ref, const uint8_t* __restrict__ other, int W, int H, size_t pitch,
-    const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
-    const uint8_t* __restrict__ valid_in, int k, uint8_t* __restrict__ disp_u8,
-    uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out) {
-    __shared__ __attribute__((aligned(16))) uint8_t Rr[PT_REG_H][PT_REG_W];   // read as dwords
-    __shared__ __attribute__((aligned(16))) uint8_t AD[PT_REG_H][PT_REG_W];
-    __shared__ unsigned Pf[PT_ROWS][PT_P_W];   // per-row exclusive prefix of column sums
-    __shared__ unsigned bits[PT_MAXBITS / 32];
-    __shared__ __attribute__((aligned(16))) uint8_t OU[PT_OU_BYTES];   // O over every plane
-    __shared__ int box[4];                    // dx_lo, dx_hi, dy_lo, dy_hi
-    const int t = threadIdx.x;
-    const int TW = PT_REG_W - 2 * k;
-    const int tx0 = k + blockIdx.x * TW, ty0 = k + blockIdx.y * PT_ROWS;
-    const int rx0 = tx0 - k, ry0 = ty0 - k;   // region origin (image coords)
-    const int RH = PT_ROWS + 2 * k;
-    // pixels of this thread: row r = t / 8, x_l in [seg*PPT, seg*PPT + PPT)
-    const int PPT = (TW + 7) / 8;
-    const int r = t >> 3, xs = (t & 7) * PPT;
-    constexpr int MAXPPT = (PT_REG_W - 2 + 7) / 8;   // k >= 1: TW <= 62
-    Line Ls[MAXPPT];
-    bool ok[MAXPPT];
-    unsigned long long best[MAXPPT];
-    if (t < 4) box[t] = (t & 1) ? -0x7fffffff : 0x7fffffff;
-    for (int i = t; i < RH * PT_REG_W; i += 256) {
-        const int v = i >> 6, u = i & 63;
-        const int gx = rx0 + u, gy = ry0 + v;
-        Rr[v][u] = (gx < W && gy < H) ? ref[(size_t)gy * pitch + gx] : 0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < MAXPPT; j++) {
-        ok[j] = false;
-        best[j] = ~0ull;
-        const int xl = xs + j, x = tx0 + xl, y = ty0 + r;
-        if (j >= PPT || xl >= TW || x >= W - k || y >= H - k) continue;
-        const size_t p = (size_t)y * W + x;
-        if (!valid_in[p] || (mask && mask[p] == 0)) continue;
-        const int4 e = ends[p];
-        ok[j] = true;
-        Ls[j] = make_line(e.x, e.y, e.z, e.w);
-        atomicMin(&box[0], min(e.x, e.z) - x);
-        atomicMax(&box[1], max(e.x, e.z) - x);
-        atomicMin(&box[2], min(e.y, e.w) - y);
-        atomicMax(&box[3], max(e.y, e.w) - y);
-    }
-    __syncthreads();
-    const int dxlo = box[0], dylo = box[2];
-    const int bw = box[1] - box[0] + 1, bh = box[3] - box[2] + 1;
-    if (box[1] < box[0]) return;             // no valid pixel in this tile
-    if ((long long)bw * bh > PT_MAXBITS) {
-        // offset box too large for the bitmap: per-pixel waves for this tile
-        const int wave = t >> 6;
-        for (int pi = wave; pi < TW * PT_ROWS; pi += 4) {
-            const int x = tx0 + pi % TW, y = ty0 + pi / TW;
-            if (x >= W - k || y >= H - k) continue;
-            const size_t p = (size_t)y * W + x;
-            if (!valid_in[p] || (mask && mask[p] == 0)) continue;
-            match_pixel_wave<ND>(ref, other, W, pitch, x, y, ends[p], k, disp_u8, disp_u16,
-                                 valid_out);
-        }
-        return;
-    }
-    const int nwords = (bw * bh + 31) >> 5;
-    for (int i = t; i < nwords; i += 256) bits[i] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < MAXPPT; j++) {
-        if (!ok[j]) continue;
-        const int x = tx0 + xs + j, y = ty0 + r;
-        for (int i = 0; i < Ls[j].n; i++) {
-            int cx, cy;
-            line_point(Ls[j], i, cx, cy);
-            const int b = (cy - y - dylo) * bw + (cx - x - dxlo);
-            atomicOr(&bits[b >> 5], 1u << (b & 31));
-        }
-    }
-    // Stage O over the union of all planes once, when it fits: rows
-    // ry0 + dylo + [0, RH + bh - 1), cols rx0 + dxlo + [0, 64 + bw - 1); the
-    // plane loop then reads only LDS.  Otherwise each plane loads O itself.
-    const int ouw = (PT_REG_W + bw - 1 + 3) & ~3, ouh = RH + bh - 1;
-    const bool staged = ouw * ouh <= PT_OU_BYTES - 8;   // slack: the realigning read may touch one dword past the region
-    if (staged) {
-        const int ox0 = rx0 + dxlo, oy0 = ry0 + dylo;
-        for (int i = t; i < ouw * ouh; i += 256) {
-            const int v = i / ouw, u = i - v * ouw;
-            const int gx = ox0 + u, gy = oy0 + v;
-            OU[i] = (gx >= 0 && gx < W && gy >= 0 && gy < H) ? other[(size_t)gy * pitch + gx] : 0;
-        }
-    }
-    __syncthreads();
-    const int cu = t & 63, cseg = t >> 6;    // column-sum thread: column, 8-row segment
-    for (int wd = 0; wd < nwords; wd++) {
-        unsigned m = bits[wd];               // uniform across the workgroup
-        while (m) {
-            const int bit = __builtin_ctz(m);
-            m &= m - 1;
-            const int b = wd * 32 + bit;
-            const int ddy = dylo + b / bw, ddx = dxlo + b % bw;
-            // (a) AD bytes of the region for this plane
-            for (int i = t; i < RH * 16; i += 256) {
-                const int v = i >> 4, u4 = (i & 15) * 4;
-                const int gx = rx0 + u4 + ddx, gy = ry0 + v + ddy;
-                unsigned o;
-                if (staged) {
-                    // bytes OU[(v + ddy - dylo) * ouw + u4 + ddx - dxlo + 0..3], realigned
-                    const int bo = (v + ddy - dylo) * ouw + u4 + (ddx - dxlo);
-                    const unsigned* w = reinterpret_cast<const unsigned*>(OU) + (bo >> 2);
-                    const unsigned sh = (unsigned)(bo & 3);
-                    o = sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
-                } else if (gy >= 0 && gy < H && gx >= 0 && gx + 3 < W) {
-                    const uint8_t* src = other + (size_t)gy * pitch + gx;
-                    const uintptr_t a = (uintptr_t)src;
-                    const unsigned* w = (const unsigned*)(a & ~(uintptr_t)3);
-                    const unsigned sh = (unsigned)(a & 3);
-                    // never read the dword after the one holding the last byte
-                    o = sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
-                } else {
-                    o = 0;
-                    for (int q = 0; q < 4; q++) {
-                        const int x = gx + q;
-                        if (gy >= 0 && gy < H && x >= 0 && x < W)
-                            o |= (unsigned)other[(size_t)gy * pitch + x] << (8 * q);
-                    }
-                }
-                const unsigned rr = *(const unsigned*)&Rr[v][u4];
-                // |o - r| per byte on even / odd bytes as u16 pairs: max - min
-                const u16x2 oe = as_v2(o & 0x00ff00ffu), oo = as_v2((o >> 8) & 0x00ff00ffu);
-                const u16x2 re = as_v2(rr & 0x00ff00ffu), ro = as_v2((rr >> 8) & 0x00ff00ffu);
-                const unsigned de = as_u32(__builtin_elementwise_max(oe, re) - vmin2(oe, re));
-                const unsigned dd = as_u32(__builtin_elementwise_max(oo, ro) - vmin2(oo, ro));
-                *(unsigned*)&AD[v][u4] = de | (dd << 8);
-            }
-            __syncthreads();
-            // (b) column sums over 2k rows (wave = 8 output rows, lane =
-            // column), each row turned into an exclusive prefix over the 64
-            // columns by a cross-lane scan, so (c) needs two reads per pixel.
-            // (Summing 2k consecutive u16 column sums per pixel instead let
-            // the compiler merge them into unaligned wide LDS loads:
-            // SQ_LDS_UNALIGNED_STALL 3.07G of 3.84G LDS cycles.)
-            {
-                const int r0 = cseg * 8;
-                unsigned sacc = 0;
-                for (int v = 0; v < 2 * k; v++) sacc += AD[r0 + v][cu];
-#pragma unroll
-                for (int rr2 = 0; rr2 < 8; rr2++) {
-                    if (rr2 > 0) {
-                        sacc += AD[r0 + rr2 - 1 + 2 * k][cu];
-                        sacc -= AD[r0 + rr2 - 1][cu];
-                    }
-                    const unsigned sc = scan64_dpp(sacc);   // inclusive over the lanes
-                    Pf[r0 + rr2][cu + 1] = sc;
-                    if (cu == 0) Pf[r0 + rr2][0] = 0;
-                }
-            }
-            __syncthreads();
-            // (c) SAD from two prefix reads, membership, first-minimum key
-#pragma unroll
-            for (int j = 0; j < MAXPPT; j++) {
-                if (!ok[j]) continue;               // ok[] implies j < PPT, xs + j < TW
-                const int xl = xs + j;
-                const unsigned sad = Pf[r][xl + 2 * k] - Pf[r][xl];
-                const int cx = tx0 + xl + ddx, cy = ty0 + r + ddy;
-                if (!on_line(Ls[j], cx, cy)) continue;
-                const unsigned long long key =
-                    ((unsigned long long)sad << 32) | (unsigned)line_index(Ls[j], cx, cy);
-                best[j] = key < best[j] ? key : best[j];
-            }
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < MAXPPT; j++) {
-        if (!ok[j]) continue;
-        const int x = tx0 + xs + j, y = ty0 + r;
-        const size_t p = (size_t)y * W + x;
-        int cx, cy;
-        line_point(Ls[j], (int)(best[j] & 0xffffffffu), cx, cy);
-        const double dx = (double)(cx - x), dy = (double)(cy - y);
-        const int dn = (int)__builtin_sqrt(dx * dx + dy * dy);       // :89
-        disp_u8[p] = (uint8_t)dn;
-        if (disp_u16) disp_u16[p] = (uint16_t)dn;
-        if (valid_out) valid_out[p] = 1;
-    }
-}
-
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
                                              0x00020000);
 }
 
-// ---- offset-plane algorithm, v2 (the one launched) --------------------------
-// Same tiles, bitmap, planes and first-minimum keys as ref_plane_kernel; what
-// changes is the layout and who does what:
+// ---- offset-plane algorithm, v2 (A/B reference for v3: SVA_REF_PLANE=2) --------
+// A tile of TW = 64 - 2k pixel columns x 32 rows, whose window-extended region
+// is exactly 64 columns wide (one lane per region column):
 //   * R, the staged O union and the AD planes are held column-major in LDS
 //     (byte (col, row) at col * stride + row, stride an odd number of dwords),
 //     so a lane that owns a column reads 4 rows per ds_read_b32 and the 2k-row
@@ -790,6 +582,437 @@ __global__ __launch_bounds__(256) void ref_plane2_kernel(
 #endif
 }
 
+// ---- offset-plane algorithm, v3 (the one launched) --------------------------
+// v2 spent most lanes on the window halo: a wave covered the 64 region
+// columns of a (64 - 2k)-pixel tile, so at k = 20 only 24 of 64 lanes owned
+// an output.  v3 gives every lane an output column:
+//   * Tile = 64 output columns x 32 rows (wave w: rows 8w..8w+7); the region
+//     is 63 + 2k columns.  Lane u owns region columns u and u + 64 (the
+//     second is real for u < 2k - 1).  The 2k-column box sum reads the
+//     inclusive scans of both through ONE ds_bpermute: source lanes below
+//     2k - 1 hold the second scan plus the first one's total, the others the
+//     first scan.
+//   * No AD plane in LDS: the 2k-row column sums are v_sad_u8 of staged O
+//     dwords (column-major, 4 rows per dword, one wave-uniform v_alignbyte)
+//     against the lane's R dwords, which stay in registers for the whole
+//     tile; rows r0+1..r0+7 follow from masked v_sad_u8 of the leaving and
+//     entering rows.  Nothing is written to LDS per plane, so the four waves
+//     run their plane loops with no barrier.
+//   * Membership is an interval test.  Planes are visited with the tile's
+//     dominant major axis innermost (row-major bitmap when most lines are
+//     Low, column-major when High).  For one outer offset the inner offsets
+//     on a pixel's line form one interval -- of length <= 1 when the pixel's
+//     own major axis is the outer one -- recomputed only when the outer
+//     offset changes.  Per plane the test is (d_in - lo) < len, and the
+//     first-minimum key is the u32 (SAD << 12 | i): SAD < 2^20 for k <= 28,
+//     i < 4096 (Mode R requires W, H < 4096).
+constexpr int P3_ROWS = 32;                          // 4 waves x 8 rows
+constexpr int P3_RW_MAX = 63 + 2 * PT_MAXK;          // region columns
+constexpr int P3_RS = 100;                           // R column stride: 25 dwords (odd)
+constexpr int P3_OU_BYTES = 36 * 1024;
+constexpr int P3_WORDS = 4096;                       // offset bitmap: 128K bits (4K diagonals)
+constexpr int P3_MAX_OUT = 1024;                     // outer offsets
+
+// Interval [lo, lo + len) of inner offsets d_in on a pixel's line at outer
+// offset d_out; the candidate index there is i = d_in + ib0.
+//   po = o_major | o_minor << 16: the pixel minus its line start along the
+//        line's major / minor axis (signed 16-bit halves);
+//   pa = a | b << 16, pn = n | major << 16 (Line fields; n = 0: no pixel);
+//   mi: the line's major axis is the inner axis; neg: minor step is -1.
+// Candidate i of a line has minor offset floor((a*i + major - 1) / b)
+// (make_line's closed form of functions.cpp:253-321).
+__device__ __forceinline__ void line_interval(int po, int pa, int pn, bool mi, bool neg,
+                                              int d_out, int& lo, int& len, int& ib0) {
+    const int o_major = (int)(short)(po & 0xffff), o_minor = po >> 16;
+    const int a = pa & 0xffff, b = (int)((unsigned)pa >> 16);
+    const int n = pn & 0xffff, mj = (int)((unsigned)pn >> 16) - 1;
+    if (mi) {
+        // i = o_major + d_in, and floor((a*i + mj) / b) must equal the
+        // candidate's minor offset tt = step * (o_minor + d_out)
+        const int u = o_minor + d_out;
+        const int tt = neg ? -u : u;
+        int ilo = 0, ihi = 0;
+        if (tt >= 0) {
+            if (a == 0) {
+                ihi = tt == 0 ? n : 0;
+            } else {
+                // i in [ceil((tt*b - mj)/a), ceil((tt*b + b - mj)/a)); the
+                // lower bound at tt = 0 is <= 0, i.e. 0 after clamping
+                const unsigned A = (unsigned)a;
+                ilo = tt == 0 ? 0 : (int)(((unsigned)(tt * b - mj) + A - 1u) / A);
+                ihi = (int)(((unsigned)(tt * b + b - mj) + A - 1u) / A);
+            }
+        }
+        ihi = ihi > n ? n : ihi;
+        len = ihi > ilo ? ihi - ilo : 0;
+        lo = ilo - o_major;
+        ib0 = o_major;
+    } else {
+        // i = o_major + d_out is fixed; one inner offset is on the line
+        const int i = o_major + d_out;
+        const bool in = (unsigned)i < (unsigned)n;
+        const int t = (b > 0 && in) ? (int)((unsigned)(a * i + mj) / (unsigned)b) : 0;
+        lo = (neg ? -t : t) - o_minor;
+        len = in ? 1 : 0;
+        ib0 = i - lo;
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void ref_plane3_kernel(
+    const uint8_t* __restrict__ ref, const uint8_t* __restrict__ other, int W, int H, size_t pitch,
+    const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
+    const uint8_t* __restrict__ valid_in, uint8_t* __restrict__ disp_u8,
+    uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out) {
+    constexpr int W2 = 2 * K;
+    constexpr int ND = (W2 + 3) / 4;          // dwords holding a 2k-row column
+    constexpr bool ODD = (W2 & 2) != 0;       // the 2k rows end mid-dword
+    constexpr int ND2 = (W2 + 6) / 4 + 1;     // dwords holding rows r0 .. r0 + 2k + 6
+    constexpr int RW = 63 + W2;
+    constexpr int RS4 = P3_RS / 4;
+    static_assert(24 + 4 * ND2 <= P3_RS, "R column stride too small");
+    static_assert(ND2 >= ND + 2, "entering rows");
+    __shared__ __attribute__((aligned(16))) uint8_t RT[P3_RW_MAX * P3_RS];
+    __shared__ unsigned bits[P3_WORDS];
+    __shared__ __attribute__((aligned(16))) uint8_t OUT[P3_OU_BYTES];
+    __shared__ short omn[P3_MAX_OUT], omx[P3_MAX_OUT];
+    __shared__ int box[6];   // dx_lo, dx_hi, dy_lo, dy_hi, #High pixels, #pixels
+    __shared__ int nuniq;
+    unsigned short* uniq = reinterpret_cast<unsigned short*>(OUT);   // before OUT is staged
+    const int t = threadIdx.x, lane = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int tx0 = K + blockIdx.x * 64, ty0 = K + blockIdx.y * P3_ROWS;
+    const int rx0 = tx0 - K, ry0 = ty0 - K;   // region origin (image coords)
+    const int r0 = 8 * wv;
+    if (t < 6) box[t] = t >= 4 ? 0 : ((t & 1) ? -0x7fffffff : 0x7fffffff);
+    // R region, column-major; rows up to the stride are staged as well (read
+    // into registers below, masked out of every sum)
+    for (int i = t; i < RW * P3_RS; i += 256) {
+        const int v = i / RW, u = i - v * RW;
+        const int gx = rx0 + u, gy = ry0 + v;
+        RT[u * P3_RS + v] = (gx < W && gy < H) ? ref[(size_t)gy * pitch + gx] : 0;
+    }
+    // this thread's pixels: column tx0 + lane, rows ty0 + r0 + j
+    int ox[8], oy[8], pa[8], pn[8];
+    bool high[8], neg[8];
+    int4 E[8];
+    {
+        unsigned vin[8], mk[8];
+        const int xc = min(tx0 + lane, W - 1);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const size_t p = (size_t)min(ty0 + r0 + j, H - 1) * W + xc;
+            vin[j] = valid_in[p];
+            mk[j] = mask ? mask[p] : 1u;
+            E[j] = ends[p];
+        }
+        int bx0 = 0x7fffffff, bx1 = -0x7fffffff, by0 = 0x7fffffff, by1 = -0x7fffffff;
+        int nh = 0, nok = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int x = tx0 + lane, y = ty0 + r0 + j;
+            const bool ok = x < W - K && y < H - K && vin[j] != 0 && mk[j] != 0;
+            const Line L = make_line(E[j].x, E[j].y, E[j].z, E[j].w);
+            high[j] = L.high != 0;
+            neg[j] = L.step < 0;
+            ox[j] = x - L.x0;
+            oy[j] = y - L.y0;
+            pa[j] = L.a | (L.b << 16);
+            pn[j] = (ok ? L.n : 0) | (L.major << 16);
+            if (ok) {
+                bx0 = min(bx0, min(E[j].x, E[j].z) - x);
+                bx1 = max(bx1, max(E[j].x, E[j].z) - x);
+                by0 = min(by0, min(E[j].y, E[j].w) - y);
+                by1 = max(by1, max(E[j].y, E[j].w) - y);
+                nh += L.high ? 1 : 0;
+                nok++;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {   // wave reductions, then one atomic each
+            bx0 = min(bx0, __shfl_xor(bx0, off, 64));
+            bx1 = max(bx1, __shfl_xor(bx1, off, 64));
+            by0 = min(by0, __shfl_xor(by0, off, 64));
+            by1 = max(by1, __shfl_xor(by1, off, 64));
+            nh += __shfl_xor(nh, off, 64);
+            nok += __shfl_xor(nok, off, 64);
+        }
+        if (lane == 0) {
+            atomicMin(&box[0], bx0);
+            atomicMax(&box[1], bx1);
+            atomicMin(&box[2], by0);
+            atomicMax(&box[3], by1);
+            atomicAdd(&box[4], nh);
+            atomicAdd(&box[5], nok);
+        }
+    }
+    __syncthreads();
+    if (box[1] < box[0]) return;             // no valid pixel in this tile
+    const int dxlo = box[0], dylo = box[2];
+    const int bw = box[1] - box[0] + 1, bh = box[3] - box[2] + 1;
+    const bool cm = 2 * box[4] > box[5];     // inner axis y: High lines dominate
+    const int n_in = cm ? bh : bw, n_out = cm ? bw : bh;
+    const int wpo = (n_in + 31) >> 5;        // bitmap words per outer offset
+    if ((long long)wpo * n_out > P3_WORDS || n_out > P3_MAX_OUT) {
+        p3_fallback:
+        // offset box too large for the bitmap (or one outer offset's O span
+        // for the staging buffer): per-pixel waves for this tile
+        for (int pi = wv; pi < 64 * P3_ROWS; pi += 4) {
+            const int x = tx0 + (pi & 63), y = ty0 + (pi >> 6);
+            if (x >= W - K || y >= H - K) continue;
+            const size_t p = (size_t)y * W + x;
+            if (!valid_in[p] || (mask && mask[p] == 0)) continue;
+            match_pixel_wave<ND>(ref, other, W, pitch, x, y, ends[p], K, disp_u8, disp_u16,
+                                 valid_out);
+        }
+        return;
+    }
+    const int nwords = wpo * n_out;
+    for (int i = t; i < nwords; i += 256) bits[i] = 0;
+    if (t == 0) nuniq = 0;
+    __syncthreads();
+    // Bresenham is translation-invariant: pixels whose endpoints, relative
+    // to themselves, match the left neighbour's or the previous row's have the
+    // same offset set.  Only the first of each such chain enters the list.
+    {
+        int4 prev = make_int4(0, 0, 0, 0);
+        bool prev_ok = false;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int x = tx0 + lane, y = ty0 + r0 + j;
+            const bool ok = (pn[j] & 0xffff) != 0;
+            const int4 rel = make_int4(E[j].x - x, E[j].y - y, E[j].z - x, E[j].w - y);
+            const int lx = __shfl_up(rel.x, 1, 64), ly = __shfl_up(rel.y, 1, 64);
+            const int lz = __shfl_up(rel.z, 1, 64), lw = __shfl_up(rel.w, 1, 64);
+            const int lok = __shfl_up((int)ok, 1, 64);
+            const bool same_left = lane > 0 && lok && lx == rel.x && ly == rel.y && lz == rel.z &&
+                                   lw == rel.w;
+            const bool same_up = prev_ok && prev.x == rel.x && prev.y == rel.y &&
+                                 prev.z == rel.z && prev.w == rel.w;
+            if (ok && !same_left && !same_up)
+                uniq[atomicAdd(&nuniq, 1)] = (unsigned short)((r0 + j) * 64 + lane);
+            prev = rel;
+            prev_ok = ok;
+        }
+    }
+    __syncthreads();
+    // one thread per distinct line, walking it incrementally (the minor
+    // offset of point i advances by at most one per step since a <= b)
+    const int bstride = wpo * 32;
+    for (int q = t; q < nuniq; q += 256) {
+        const int pl = uniq[q], x = tx0 + (pl & 63), y = ty0 + (pl >> 6);
+        const int4 e = ends[(size_t)y * W + x];
+        const Line L = make_line(e.x, e.y, e.z, e.w);
+        int mnr = L.b > 0 ? (L.major - 1) / L.b : 0;
+        int rem = L.b > 0 ? (L.major - 1) - mnr * L.b : 0;
+        const int bx0 = L.x0 - x - dxlo, by0 = L.y0 - y - dylo;
+        for (int i = 0; i < L.n; i++) {
+            const int off = L.step * mnr;
+            const int rx = L.high ? bx0 + off : bx0 + i;
+            const int ry = L.high ? by0 + i : by0 + off;
+            const int b = cm ? rx * bstride + ry : ry * bstride + rx;
+            atomicOr(&bits[b >> 5], 1u << (b & 31));
+            rem += L.a;
+            if (rem >= L.b) {
+                rem -= L.b;
+                mnr++;
+            }
+        }
+    }
+    __syncthreads();
+    // Per outer offset, the first and last inner offset with a plane.  The
+    // planes are staged in chunks of consecutive outer offsets whose O
+    // rectangle fits OUT (one chunk for Low/High pairs at 1080p; diagonal
+    // pairs, whose offset box is a thin diagonal band, take a few); an outer
+    // offset whose inner span alone does not fit is split into windows.
+    auto stage_bytes = [&](int span_out, int span_in) {
+        const int cw = RW + (cm ? span_out : span_in) - 1;
+        const int ch = 24 + (cm ? span_in : span_out) - 1 + 4 * (ND2 + 1);
+        return cw * ((((ch + 3) >> 2) | 1) << 2);
+    };
+    for (int o = t; o < n_out; o += 256) {
+        int mn = 0x7fff, mx = -1;
+        for (int wc = 0; wc < wpo; wc++) {
+            const unsigned m = bits[o * wpo + wc];
+            if (m) {
+                mn = min(mn, wc * 32 + __builtin_ctz(m));
+                mx = max(mx, wc * 32 + 31 - __builtin_clz(m));
+            }
+        }
+        omn[o] = (short)mn;
+        omx[o] = (short)mx;
+    }
+    if (stage_bytes(1, 1) > P3_OU_BYTES) goto p3_fallback;   // uniform (k, box)
+    // widest inner window of a single outer offset
+    int iwmax = 1;
+    for (int step = 1 << 12; step; step >>= 1)
+        if (iwmax + step <= n_in && stage_bytes(1, iwmax + step) <= P3_OU_BYTES) iwmax += step;
+    __syncthreads();
+
+    // R dwords of this lane's two region columns, rows r0 .. r0 + 4*ND2 - 1
+    const int ca = lane, cb = min(lane + 64, RW - 1);
+    unsigned RA[ND2], RB[ND2];
+    {
+        const unsigned* RT32 = reinterpret_cast<const unsigned*>(RT);
+#pragma unroll
+        for (int q = 0; q < ND2; q++) {
+            RA[q] = RT32[ca * RS4 + (r0 >> 2) + q];
+            RB[q] = RT32[cb * RS4 + (r0 >> 2) + q];
+        }
+    }
+    // rows r0 + 2k .. r0 + 2k + 7 (the rows entering the window)
+    auto entering = [](const unsigned (&X)[ND2], int e) -> unsigned {
+        return ODD ? __builtin_amdgcn_alignbyte(X[ND + e], X[ND - 1 + e], 2) : X[ND + e];
+    };
+    const unsigned reA0 = entering(RA, 0), reA1 = entering(RA, 1);
+    const unsigned reB0 = entering(RB, 0), reB1 = entering(RB, 1);
+    // column sums of |O - R| over rows [r0 + j, r0 + j + 2k), j < 8, for one
+    // region column whose O dwords start at byte ob of OUT
+    auto colsums = [&](const unsigned (&R)[ND2], unsigned re0, unsigned re1, int ob,
+                       unsigned (&cs)[8]) {
+        const unsigned* w = reinterpret_cast<const unsigned*>(OUT) + (ob >> 2);
+        const unsigned sh = (unsigned)(ob & 3);
+        unsigned raw[ND2 + 1], O[ND2];
+#pragma unroll
+        for (int q = 0; q <= ND2; q++) raw[q] = w[q];
+#pragma unroll
+        for (int q = 0; q < ND2; q++) O[q] = __builtin_amdgcn_alignbyte(raw[q + 1], raw[q], sh);
+        unsigned s0 = 0;
+#pragma unroll
+        for (int q = 0; q < ND; q++) {
+            unsigned o = O[q], r = R[q];
+            if (ODD && q == ND - 1) { o &= 0xffffu; r &= 0xffffu; }
+            s0 = __builtin_amdgcn_sad_u8(o, r, s0);
+        }
+        const unsigned oe0 = entering(O, 0), oe1 = entering(O, 1);
+        // X_j = sum of the j rows leaving, E_j = s0 + sum of the j rows entering
+        const unsigned x4 = __builtin_amdgcn_sad_u8(O[0], R[0], 0u);
+        const unsigned e4 = __builtin_amdgcn_sad_u8(oe0, re0, s0);
+        cs[0] = s0;
+        cs[4] = e4 - x4;
+#pragma unroll
+        for (int j = 1; j < 4; j++) {
+            const unsigned m = (1u << (8 * j)) - 1u;
+            const unsigned xj = __builtin_amdgcn_sad_u8(O[0] & m, R[0] & m, 0u);
+            const unsigned ej = __builtin_amdgcn_sad_u8(oe0 & m, re0 & m, s0);
+            cs[j] = ej - xj;
+            const unsigned xk = __builtin_amdgcn_sad_u8(O[1] & m, R[1] & m, x4);
+            const unsigned ek = __builtin_amdgcn_sad_u8(oe1 & m, re1 & m, e4);
+            cs[4 + j] = ek - xk;
+        }
+    };
+
+    unsigned best[8];
+    int lo[8], len[8], ib0[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        best[j] = 0xffffffffu;
+        lo[j] = len[j] = ib0[j] = 0;
+    }
+    // line offsets along each line's own axes (see line_interval)
+    int po[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const int omaj = high[j] ? oy[j] : ox[j], omin = high[j] ? ox[j] : oy[j];
+        po[j] = (omaj & 0xffff) | (omin << 16);
+    }
+    const int in_lo = cm ? dylo : dxlo, out_lo = cm ? dxlo : dylo;
+    const int src = ((lane + W2 - 1) & 63) << 2;
+    for (int o0 = 0, wst = -1;;) {           // wst >= 0: outer offset o0 continues there
+        if (wst < 0) {
+            while (o0 < n_out && __builtin_amdgcn_readfirstlane(omn[o0] > omx[o0])) o0++;
+            if (o0 >= n_out) break;
+        }
+        int o1 = o0 + 1;
+        int ilo = __builtin_amdgcn_readfirstlane(omn[o0]);
+        int ihi = __builtin_amdgcn_readfirstlane(omx[o0]);
+        if (wst >= 0 || ihi - ilo + 1 > iwmax) {
+            // one outer offset, inner window [ilo, ihi]
+            const int end = ihi;
+            ilo = wst >= 0 ? wst : ilo;
+            ihi = min(end, ilo + iwmax - 1);
+            wst = ihi < end ? ihi + 1 : -1;
+        } else {
+            // grow the chunk [o0, o1) while its O rectangle fits
+            for (; o1 < n_out; o1++) {
+                const int a = __builtin_amdgcn_readfirstlane(omn[o1]);
+                const int b = __builtin_amdgcn_readfirstlane(omx[o1]);
+                const int nl = a <= b ? min(ilo, a) : ilo, nh = a <= b ? max(ihi, b) : ihi;
+                if (stage_bytes(o1 + 1 - o0, nh - nl + 1) > P3_OU_BYTES) break;
+                ilo = nl;
+                ihi = nh;
+            }
+        }
+        // O over the chunk: columns rx0 + dxb + [0, ouw), rows ry0 + dyb +
+        // [0, ouh) (every dword a plane reads), column stride os (odd dwords)
+        const int dxb = cm ? out_lo + o0 : in_lo + ilo, dyb = cm ? in_lo + ilo : out_lo + o0;
+        const int ouw = RW + (cm ? o1 - o0 : ihi - ilo + 1) - 1;
+        const int ouh = 24 + (cm ? ihi - ilo + 1 : o1 - o0) - 1 + 4 * (ND2 + 1);
+        const int os = ((((ouh + 3) >> 2) | 1) << 2);
+        __syncthreads();                     // the previous chunk's planes are done
+        {
+            const int ox0 = rx0 + dxb, oy0 = ry0 + dyb;
+            for (int i = t; i < ouw * ouh; i += 256) {
+                const int v = i / ouw, u = i - v * ouw;
+                const int gx = ox0 + u, gy = oy0 + v;
+                OUT[u * os + v] = (gx >= 0 && gx < W && gy >= 0 && gy < H)
+                                      ? other[(size_t)gy * pitch + gx] : 0;
+            }
+        }
+        __syncthreads();
+        for (int ot = o0; ot < o1; ot++) {
+            const int d_out = out_lo + ot;
+            const int wlo = max(ilo, __builtin_amdgcn_readfirstlane(omn[ot]));
+            const int whi = min(ihi, __builtin_amdgcn_readfirstlane(omx[ot]));
+            if (wlo > whi) continue;
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                line_interval(po[j], pa[j], pn[j], high[j] == cm, neg[j], d_out, lo[j], len[j],
+                              ib0[j]);
+            for (int wc = wlo >> 5; wc <= (whi >> 5); wc++) {
+                unsigned m = (unsigned)__builtin_amdgcn_readfirstlane((int)bits[ot * wpo + wc]);
+                if (wc == (wlo >> 5)) m &= ~0u << (wlo & 31);            // window edges
+                if (wc == (whi >> 5)) m &= ~0u >> (31 - (whi & 31));
+                while (m) {
+                    const int d_in = in_lo + wc * 32 + __builtin_ctz(m);
+                    m &= m - 1;
+                    const int ddx = cm ? d_out : d_in, ddy = cm ? d_in : d_out;
+                    const int ob = (ddx - dxb) * os + (ddy - dyb) + r0;
+                    unsigned csA[8], csB[8];
+                    colsums(RA, reA0, reA1, ob + ca * os, csA);
+                    colsums(RB, reB0, reB1, ob + cb * os, csB);
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const unsigned Pa = scan64_dpp(csA[j]), Pb = scan64_dpp(csB[j]);
+                        const unsigned ta = (unsigned)__builtin_amdgcn_readlane((int)Pa, 63);
+                        const unsigned V = lane < W2 - 1 ? Pb + ta : Pa;
+                        const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)V);
+                        const unsigned sad = hi - Pa + csA[j];
+                        const unsigned key = (sad << 12) | (unsigned)(d_in + ib0[j]);
+                        const bool on = (unsigned)(d_in - lo[j]) < (unsigned)len[j];
+                        best[j] = on ? min(best[j], key) : best[j];
+                    }
+                }
+            }
+        }
+        if (wst < 0) o0 = o1;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        if ((pn[j] & 0xffff) == 0) continue;
+        const int x = tx0 + lane, y = ty0 + r0 + j;
+        const size_t p = (size_t)y * W + x;
+        const int4 e = ends[p];
+        int cx, cy;
+        line_point(make_line(e.x, e.y, e.z, e.w), (int)(best[j] & 0xfffu), cx, cy);
+        const double dx = (double)(cx - x), dy = (double)(cy - y);
+        const int dn = (int)__builtin_sqrt(dx * dx + dy * dy);       // :89
+        disp_u8[p] = (uint8_t)dn;
+        if (disp_u16) disp_u16[p] = (uint16_t)dn;
+        if (valid_out) valid_out[p] = 1;
+    }
+}
+
 __global__ void disp_to_depth_kernel(const uint8_t* __restrict__ disp, int n, double num,
                                      double pixel_size, double* __restrict__ depth) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -825,31 +1048,50 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
     const long long npx = (long long)(W - 2 * k) * (H - 2 * k);
     if (npx <= 0) return hipSuccess;
     if (k <= PT_MAXK) {   // offset-plane algorithm
-        const int tw = PT_REG_W - 2 * k;
-        const dim3 pg((unsigned)((W - 2 * k + tw - 1) / tw), (unsigned)((H - 2 * k + PT_ROWS - 1) / PT_ROWS));
-        const dim3 pg2((unsigned)((W - 2 * k + tw - 1) / tw),
-                       (unsigned)((H - 2 * k + P2_ROWS - 1) / P2_ROWS));
         // A/B switch for the previous plane kernel (tools/bench_refpath.py)
-        static const bool plane_v1 = getenv("SVA_REF_PLANE_V1") != nullptr;
-#define SVA_PLANE_CASE(ND)                                                                     \
+        static const bool plane_v2 = [] {
+            const char* e = getenv("SVA_REF_PLANE");
+            return e && e[0] == '2';
+        }();
+        if (plane_v2) {
+            const int tw = PT_REG_W - 2 * k;
+            const dim3 pg2((unsigned)((W - 2 * k + tw - 1) / tw),
+                           (unsigned)((H - 2 * k + P2_ROWS - 1) / P2_ROWS));
+#define SVA_PLANE2_CASE(ND)                                                                    \
     case ND:                                                                                   \
-        if (plane_v1)                                                                          \
-            hipLaunchKernelGGL(ref_plane_kernel<ND>, pg, dim3(256), 0, c.stream, ref, other, W, \
-                               H, pitch, mask, (const int4*)ends, valid_in, k, disp_u8,         \
-                               disp_u16, valid_out);                                            \
-        else                                                                                   \
-            hipLaunchKernelGGL(ref_plane2_kernel<ND>, pg2, dim3(256), 0, c.stream, ref, other,  \
-                               W, H, pitch, mask, (const int4*)ends, valid_in, k, disp_u8,      \
-                               disp_u16, valid_out);                                            \
+        hipLaunchKernelGGL(ref_plane2_kernel<ND>, pg2, dim3(256), 0, c.stream, ref, other, W, H, \
+                           pitch, mask, (const int4*)ends, valid_in, k, disp_u8, disp_u16,      \
+                           valid_out);                                                         \
         break;
-        switch ((k + 1) / 2) {
-            SVA_PLANE_CASE(1) SVA_PLANE_CASE(2) SVA_PLANE_CASE(3) SVA_PLANE_CASE(4)
-            SVA_PLANE_CASE(5) SVA_PLANE_CASE(6) SVA_PLANE_CASE(7) SVA_PLANE_CASE(8)
-            SVA_PLANE_CASE(9) SVA_PLANE_CASE(10) SVA_PLANE_CASE(11) SVA_PLANE_CASE(12)
-            SVA_PLANE_CASE(13) SVA_PLANE_CASE(14)
+            switch ((k + 1) / 2) {
+                SVA_PLANE2_CASE(1) SVA_PLANE2_CASE(2) SVA_PLANE2_CASE(3) SVA_PLANE2_CASE(4)
+                SVA_PLANE2_CASE(5) SVA_PLANE2_CASE(6) SVA_PLANE2_CASE(7) SVA_PLANE2_CASE(8)
+                SVA_PLANE2_CASE(9) SVA_PLANE2_CASE(10) SVA_PLANE2_CASE(11) SVA_PLANE2_CASE(12)
+                SVA_PLANE2_CASE(13) SVA_PLANE2_CASE(14)
+                default: return hipErrorInvalidValue;
+            }
+#undef SVA_PLANE2_CASE
+            return hipGetLastError();
+        }
+        const dim3 pg3((unsigned)((W - 2 * k + 63) / 64),
+                       (unsigned)((H - 2 * k + P3_ROWS - 1) / P3_ROWS));
+#define SVA_PLANE3_CASE(K_)                                                                    \
+    case K_:                                                                                   \
+        hipLaunchKernelGGL(ref_plane3_kernel<K_>, pg3, dim3(256), 0, c.stream, ref, other, W, H, \
+                           pitch, mask, (const int4*)ends, valid_in, disp_u8, disp_u16,         \
+                           valid_out);                                                         \
+        break;
+        switch (k) {
+            SVA_PLANE3_CASE(1) SVA_PLANE3_CASE(2) SVA_PLANE3_CASE(3) SVA_PLANE3_CASE(4)
+            SVA_PLANE3_CASE(5) SVA_PLANE3_CASE(6) SVA_PLANE3_CASE(7) SVA_PLANE3_CASE(8)
+            SVA_PLANE3_CASE(9) SVA_PLANE3_CASE(10) SVA_PLANE3_CASE(11) SVA_PLANE3_CASE(12)
+            SVA_PLANE3_CASE(13) SVA_PLANE3_CASE(14) SVA_PLANE3_CASE(15) SVA_PLANE3_CASE(16)
+            SVA_PLANE3_CASE(17) SVA_PLANE3_CASE(18) SVA_PLANE3_CASE(19) SVA_PLANE3_CASE(20)
+            SVA_PLANE3_CASE(21) SVA_PLANE3_CASE(22) SVA_PLANE3_CASE(23) SVA_PLANE3_CASE(24)
+            SVA_PLANE3_CASE(25) SVA_PLANE3_CASE(26) SVA_PLANE3_CASE(27) SVA_PLANE3_CASE(28)
             default: return hipErrorInvalidValue;
         }
-#undef SVA_PLANE_CASE
+#undef SVA_PLANE3_CASE
         return hipGetLastError();
     }
     dim3 grid((unsigned)((npx + 3) / 4));

@@ -65,13 +65,17 @@ def test_ref_path_pairs(ctx, sva, oracle, pair):
     assert np.array_equal(d16, o16)
 
 
-@pytest.mark.parametrize("k", [1, 3, 8, 20, 21, 32])
-def test_ref_path_window_sizes(ctx, sva, oracle, k):
-    """Windows 2k x 2k incl. odd k (2k % 4 == 2: partial last dword)."""
+@pytest.mark.parametrize("pair", [(12, 11), (12, 7)])
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 8, 13, 20, 21, 27, 28, 29, 32])
+def test_ref_path_window_sizes(ctx, sva, oracle, k, pair):
+    """Windows 2k x 2k incl. odd k (2k % 4 == 2: partial last dword), every
+    row-count class of the plane kernel (k <= 28, one instantiation per k)
+    and the per-pixel kernel above it; Low (12 -> 11) and High (12 -> 7)
+    lines, i.e. both plane orders."""
     W, H = 200, 150
-    cr, co, ocr, oco = cams_for(sva, oracle, W, 12, 11)
+    cr, co, ocr, oco = cams_for(sva, oracle, W, *pair)
     a = synth.texture(H, W, k)
-    b = np.roll(a, 10, axis=1)
+    b = np.roll(a, 10, axis=1 if pair[1] == 11 else 0)
     d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k)
     o8, o16, ovalid, _ = oracle.ref_pair(a, b, ocr, oco, k=k)
     assert np.array_equal(valid, ovalid) and np.array_equal(d16, o16)
@@ -203,6 +207,30 @@ def test_ref_path_1080p_row_sampled(ctx, sva, oracle, pair):
     mask[MODE_R_1080P_ROWS, :] = 1
     d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k, mask=mask)
     o8, o16, ov = _oracle_rows(oracle, a, b, ocr, oco, k, MODE_R_1080P_ROWS, W, H)
+    assert ov.sum() > 0.3 * mask.sum()
+    assert np.array_equal(valid, ov)
+    assert np.array_equal(d16, o16)
+    assert np.array_equal(d8, o8)
+
+
+# 4K (BASELINE config 3's size): the v3 plane kernel stages O in chunks of
+# outer offsets (diagonal pairs) and splits one outer offset's inner span into
+# windows (High lines, 12 -> 7); 12 full-width rows per pair.
+MODE_R_4K_ROWS = np.linspace(20, 2160 - 21, 12).astype(int)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("pair", [(12, 11), (12, 7), (12, 6), (12, 18)])
+def test_ref_path_4k_row_sampled(ctx, sva, oracle, pair):
+    W, H, k = 3840, 2160, 20
+    cr, co, ocr, oco = cams_for(sva, oracle, W, *pair)
+    a = synth.texture(H, W, 60 + pair[1])
+    gx, gy = pair[1] % 5 - 2, pair[1] // 5 - 2
+    b = np.roll(np.roll(a, -356 * gy, axis=0), -356 * gx, axis=1)
+    mask = np.zeros((H, W), np.uint8)
+    mask[MODE_R_4K_ROWS, :] = 1
+    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k, mask=mask)
+    o8, o16, ov = _oracle_rows(oracle, a, b, ocr, oco, k, MODE_R_4K_ROWS, W, H, chunks=12)
     assert ov.sum() > 0.3 * mask.sum()
     assert np.array_equal(valid, ov)
     assert np.array_equal(d16, o16)

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--sizes", default="640x480,1920x1080")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu-rows", type=int, default=24, help="rows of the CPU sample")
+    ap.add_argument("--pairs", default="12-11", help="reference-rig pairs, e.g. 12-11,12-7,12-6")
     a = ap.parse_args()
     import torch
     import stereovisionarray_amd as sva
@@ -36,12 +37,14 @@ def main():
     torch.cuda.set_stream(s)
     ctx.set_stream(s.cuda_stream)
     out = []
-    for spec in a.sizes.split(","):
+    import hashlib
+    for spec, pair in [(s_, p_) for s_ in a.sizes.split(",") for p_ in a.pairs.split(",")]:
         W, H = map(int, spec.split("x"))
+        i_ref, i_oth = map(int, pair.split("-"))
         k = 20
         grid = synth.reference_array(0.036 / W)
-        cr, co = sva.Camera.make(*grid[12]), sva.Camera.make(*grid[11])
-        ocr, oco = pyoracle.OCamera.make(*grid[12]), pyoracle.OCamera.make(*grid[11])
+        cr, co = sva.Camera.make(*grid[i_ref]), sva.Camera.make(*grid[i_oth])
+        ocr, oco = pyoracle.OCamera.make(*grid[i_ref]), pyoracle.OCamera.make(*grid[i_oth])
         ref = synth.texture(H, W, 5)
         shift = int(round(0.05 * 0.05 / 1.0 / (0.036 / W) * 1.5))  # ~ mid-range disparity
         oth = np.roll(ref, shift, axis=1)
@@ -82,7 +85,9 @@ def main():
         cdt = time.perf_counter() - t0
         cpu_rate = ncpu / cdt / 1e6
         del band
-        out.append({"size": f"{W}x{H}", "candidates": int(n_cand), "gpu_ms": round(dt * 1e3, 3),
+        digest = hashlib.sha1(d16.cpu().numpy().tobytes() + val.cpu().numpy().tobytes()).hexdigest()[:16]
+        out.append({"size": f"{W}x{H}", "pair": pair, "plane_kernel": os.environ.get("SVA_REF_PLANE", "3"),
+                    "out_sha1": digest, "candidates": int(n_cand), "gpu_ms": round(dt * 1e3, 3),
                     "ref_match_ms": round(ms_match / max(n, 1), 3),
                     "gpu_Mcand_per_s": round(gpu_rate, 1),
                     "cpu_Mcand_per_s_1thread": round(cpu_rate, 3),
