@@ -122,31 +122,11 @@ __global__ __launch_bounds__(TX* TY) void census9x7_rows_kernel(
             if (x >= HX && x < W - HX && y >= HY && y < H - HY) {
                 // the window of lane tx is ring bytes [tx, tx+8]: three aligned
                 // dwords per row, realigned with v_alignbyte (no unaligned LDS)
-                const int base = threadIdx.x >> 2;
-                const unsigned sh = threadIdx.x & 3;
-                const unsigned* crow = reinterpret_cast<const unsigned*>(ring[y & (RING - 1)]);
-                const int c = (int)(__builtin_amdgcn_alignbyte(crow[base + 2], crow[base + 1], sh) & 0xff);
-                unsigned hi = 0, lo = 0;
-                int e = 0;
+                const unsigned* rows[7];
 #pragma unroll
-                for (int dy = -HY; dy <= HY; dy++) {
-                    const unsigned* row = reinterpret_cast<const unsigned*>(ring[(y + dy) & (RING - 1)]);
-                    const unsigned w0 = row[base], w1 = row[base + 1], w2 = row[base + 2];
-                    const unsigned a[3] = {__builtin_amdgcn_alignbyte(w1, w0, sh),
-                                           __builtin_amdgcn_alignbyte(w2, w1, sh),
-                                           __builtin_amdgcn_alignbyte(w2, w2, sh)};
-#pragma unroll
-                    for (int dx = -HX; dx <= HX; dx++) {
-                        if (dx == 0 && dy == 0) continue;
-                        const int i = dx + HX;
-                        const int n = (int)((a[i >> 2] >> (8 * (i & 3))) & 0xff);
-                        // (hi << 1) | sign(n - c): bit = n < c
-                        if (e < 30) hi = __builtin_amdgcn_alignbit(hi, (unsigned)(n - c), 31);
-                        else lo = __builtin_amdgcn_alignbit(lo, (unsigned)(n - c), 31);
-                        e++;
-                    }
-                }
-                word = ((uint64_t)hi << 32) | lo;
+                for (int dy = -HY; dy <= HY; dy++)
+                    rows[dy + HY] = reinterpret_cast<const unsigned*>(ring[(y + dy) & (RING - 1)]);
+                word = census9x7(rows, threadIdx.x >> 2, threadIdx.x & 3);
             }
             uint64_t* orow = out + (size_t)y * ostride;
             orow[x] = word;

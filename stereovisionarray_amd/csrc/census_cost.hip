@@ -39,33 +39,9 @@ __device__ __forceinline__ void store16_nt(uint8_t* p, const unsigned (&o)[4]) {
 }
 
 // Census word of the pixel whose 9-byte window row starts at byte s of each
-// ring row; `rows[dy+3]` are the dword views of ring rows y-3 .. y+3.  Bit
-// order: row-major window, centre skipped, first element in bit 61.
+// ring row; `rows[dy+3]` are the dword views of ring rows y-3 .. y+3.
 __device__ __forceinline__ uint64_t census_at(const unsigned* const* rows, int s) {
-    const int base = s >> 2;
-    const unsigned sh = s & 3;
-    const unsigned* crow = rows[HY];
-    const int c = (int)(__builtin_amdgcn_alignbyte(crow[base + 2], crow[base + 1], sh) & 0xff);
-    unsigned hi = 0, lo = 0;
-    int e = 0;
-#pragma unroll
-    for (int dy = -HY; dy <= HY; dy++) {
-        const unsigned* row = rows[dy + HY];
-        const unsigned w0 = row[base], w1 = row[base + 1], w2 = row[base + 2];
-        const unsigned a[3] = {__builtin_amdgcn_alignbyte(w1, w0, sh),
-                               __builtin_amdgcn_alignbyte(w2, w1, sh),
-                               __builtin_amdgcn_alignbyte(w2, w2, sh)};
-#pragma unroll
-        for (int dx = -HX; dx <= HX; dx++) {
-            if (dx == 0 && dy == 0) continue;
-            const int i = dx + HX;
-            const int n = (int)((a[i >> 2] >> (8 * (i & 3))) & 0xff);
-            if (e < 30) hi = __builtin_amdgcn_alignbit(hi, (unsigned)(n - c), 31);
-            else lo = __builtin_amdgcn_alignbit(lo, (unsigned)(n - c), 31);
-            e++;
-        }
-    }
-    return ((uint64_t)hi << 32) | lo;
+    return census9x7(rows, s >> 2, (unsigned)(s & 3));
 }
 
 template <int NC>

@@ -102,4 +102,37 @@ __device__ __forceinline__ unsigned sad_row(const uint8_t* a, const uint8_t* b, 
     return acc;
 }
 
+// 9x7 Census word in the oracle's bit
+// order: element e (row-major over the window, centre skipped) at bit 61 - e,
+// bit = neighbour < centre.  rows[0..6] are dword views of image rows y-3..y+3
+// whose 9-byte window row starts at byte 4*base + sh.  Each window row is its
+// own chain of 8-9 dependent (acc << 1) | sign(n - c) steps (one
+// v_sub_u32_sdwa + v_alignbit each); the seven chains are independent and
+// are merged with shifts at the end (one 62-long chain stalled on issue).
+__device__ __forceinline__ uint64_t census9x7(const unsigned* const* rows, int base, unsigned sh) {
+    const unsigned* crow = rows[3];
+    const int c = (int)(__builtin_amdgcn_alignbyte(crow[base + 2], crow[base + 1], sh) & 0xff);
+    unsigned P[7];
+#pragma unroll
+    for (int r = 0; r < 7; r++) {
+        const unsigned* row = rows[r];
+        const unsigned w0 = row[base], w1 = row[base + 1], w2 = row[base + 2];
+        const unsigned a[3] = {__builtin_amdgcn_alignbyte(w1, w0, sh),
+                               __builtin_amdgcn_alignbyte(w2, w1, sh),
+                               __builtin_amdgcn_alignbyte(w2, w2, sh)};
+        unsigned acc = 0;
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            if (r == 3 && i == 4) continue;
+            const int n = (int)((a[i >> 2] >> (8 * (i & 3))) & 0xff);
+            acc = __builtin_amdgcn_alignbit(acc, (unsigned)(n - c), 31);
+        }
+        P[r] = acc;
+    }
+    // rows start at elements 0, 9, 18, 27 (centre row: 8), 35, 44, 53
+    const unsigned lo = (P[6] | (P[5] << 9)) | ((P[4] << 18) | (P[3] << 27));
+    const unsigned hi = ((P[3] >> 5) | (P[2] << 3)) | ((P[1] << 12) | (P[0] << 21));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 }  // namespace sva
