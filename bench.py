@@ -69,8 +69,8 @@ def parse():
                          "own HIP stream and workspaces, so pairs overlap (0 = auto: 2 when a "
                          "rank has several pairs per step, else 1)")
     ap.add_argument("--path-kernel", default="auto", choices=["auto", "cost_volume", "fused"],
-                    help="sva_set_path_kernel (DESIGN.md §4.5); auto = the library's choice on "
-                         "one stream (fused for D=256), fused when pairs overlap on streams")
+                    help="sva_set_path_kernel (DESIGN.md §4.5); auto = the library's choice "
+                         "(the cost-volume route)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="gather each step's maps synchronously on the compute stream")
     ap.add_argument("--rehearse-overlap", action="store_true",
@@ -630,8 +630,6 @@ def main():
     params = sva.default_params(D=D, dmin=0, dir=-1, subpixel=1)
     n_streams = a.streams if a.streams > 0 else (2 if P > 1 else 1)
     path_kernel = a.path_kernel
-    if path_kernel == "auto" and n_streams > 1:
-        path_kernel = "fused"        # measured: fused + overlap beats both on one stream
     kern = {"auto": sva.SVA_PATH_KERNEL_AUTO, "cost_volume": sva.SVA_PATH_KERNEL_COST_VOLUME,
             "fused": sva.SVA_PATH_KERNEL_FUSED}[path_kernel]
     ctx = sva.Context(local)
@@ -758,8 +756,7 @@ def main():
                    "parallelism": f"pairs sharded over {world} rank(s), RCCL gather to rank 0"
                                   + (" overlapped with the next step" if nbuf == 2 else ""),
                    "streams_per_rank": len(ctxs),
-                   "path_kernel": path_kernel if path_kernel != "auto" else
-                   ("fused" if D == 256 else "cost_volume")},
+                   "path_kernel": path_kernel if path_kernel != "auto" else "cost_volume"},
         "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
         "roofline": roofline,
         "cpu_baseline": None,

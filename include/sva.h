@@ -102,9 +102,10 @@ int sva_reserve(void* ctx, int width, int height, int D);
  *   (16 B/disp of HBM traffic in the path kernel).
  * FUSED: the path kernel forms the Hamming costs in registers from the census
  *   maps (8 B/disp, no cost volume, more VALU per disparity).
- * AUTO (default): FUSED for D = 256, COST_VOLUME otherwise -- the faster one on
- *   a single stream as measured on MI355X.  FUSED is also the
- *   faster choice for any D when frames overlap on two streams.
+ * AUTO (default): COST_VOLUME.  Since the cost-volume route writes only six
+ *   path volumes and recomputes the horizontal paths in its WTA kernel
+ *    it is the faster one for every D, on one stream and with
+ *   frames overlapping on two.
  * Results are identical.  2-D array steps always use the cost volume. */
 #define SVA_PATH_KERNEL_COST_VOLUME 0
 #define SVA_PATH_KERNEL_FUSED 1

@@ -406,6 +406,95 @@ inline std::vector<double> fuseDepth(Engine& eng, const std::vector<std::vector<
     return depth;
 }
 
+// ---- multi-GPU engine (sva.h "multi-GPU engine") ----------
+
+// RAII owner of an sva_multi engine: pairs shard over `devices` (pair j ->
+// devices[j mod n]) and over each device's streams; maps are gathered to
+// devices[0] by RCCL (default) or peer copies (SVA_MULTI_GATHER_PEER).
+class MultiEngine {
+public:
+    explicit MultiEngine(const std::vector<int>& devices, int streamsPerDevice = 2,
+                         int flags = SVA_MULTI_GATHER_RCCL) {
+        int s = sva_multi_create(devices.data(), (int)devices.size(), streamsPerDevice, flags, &m_);
+        if (s != SVA_OK) throw Error(s, std::string("sva_multi_create: ") + sva_status_string(s));
+    }
+    ~MultiEngine() {
+        if (m_) sva_multi_destroy(m_);
+    }
+    MultiEngine(const MultiEngine&) = delete;
+    MultiEngine& operator=(const MultiEngine&) = delete;
+    void* handle() const { return m_; }
+    void check(int s) const {
+        if (s != SVA_OK) throw Error(s, sva_multi_last_error(m_));
+    }
+    void synchronize() { check(sva_multi_synchronize(m_)); }
+
+private:
+    void* m_ = nullptr;
+};
+
+// One camera-array frame over a MultiEngine: replaces the pair loop of
+// CameraStereoVision.cpp:55 for Mode S.  Every pair (getCameraPairs,
+// functions.cpp:148-213) is matched along its own grid step (pairStep) with
+// base parameters p; the maps of each reference camera are fused into one
+// median depth map, in the order reference cameras first
+// appear in `pairs`.  All images share width, height and pitch; f and
+// pixel_size are the first reference camera's.  maps (nullable) receives
+// every pair's u16 map in `pairs` order.
+inline std::vector<std::vector<double>> computeArrayDepth(
+    MultiEngine& m, const std::vector<ImageView>& images, const std::vector<Camera>& cameras,
+    const std::vector<std::array<int, 2>>& pairs, const sva_sgm_params& p, double pitch = 0.05,
+    std::vector<std::vector<uint16_t>>* maps = nullptr) {
+    if (pairs.empty()) throw Error(SVA_ERR_INVALID_ARG, "computeArrayDepth: no camera pairs");
+    const ImageView& first = images.at(pairs[0][0]);
+    const int W = first.width, H = first.height;
+    for (const auto& im : images)
+        if (im.width != W || im.height != H || im.pitch != first.pitch)
+            throw Error(SVA_ERR_INVALID_ARG, "computeArrayDepth: images differ in size");
+    // group the pairs by reference camera (stable: first appearance order)
+    std::vector<int> refs;
+    for (const auto& pr : pairs)
+        if (std::find(refs.begin(), refs.end(), pr[0]) == refs.end()) refs.push_back(pr[0]);
+    std::vector<sva_array_pair> ap;
+    std::vector<int32_t> group_start;
+    std::vector<size_t> order;   // ap index -> index in pairs
+    for (int r : refs) {
+        group_start.push_back((int32_t)ap.size());
+        for (size_t j = 0; j < pairs.size(); j++) {
+            if (pairs[j][0] != r) continue;
+            const PairStep st = pairStep(cameras.at(pairs[j][0]), cameras.at(pairs[j][1]), pitch);
+            sva_array_pair a;
+            a.ref = pairs[j][0];
+            a.other = pairs[j][1];
+            a.params = p;
+            a.params.dir = st.dir;
+            a.params.dir_y = st.dir_y;
+            a.baseline = st.baseline;
+            ap.push_back(a);
+            order.push_back(j);
+        }
+    }
+    group_start.push_back((int32_t)ap.size());
+    std::vector<const uint8_t*> ptrs;
+    for (const auto& im : images) ptrs.push_back(im.data);
+    const size_t np = (size_t)W * H;
+    const int ng = (int)refs.size();
+    std::vector<double> depth(np * ng);
+    std::vector<uint16_t> all(maps ? np * ap.size() : 0);
+    const Camera& c0 = cameras.at(refs[0]);
+    m.check(sva_array_depth(m.handle(), ptrs.data(), (int)ptrs.size(), W, H, first.pitch, ap.data(),
+                            (int)ap.size(), group_start.data(), ng, c0.f, c0.pixel_size,
+                            depth.data(), nullptr, maps ? all.data() : nullptr));
+    if (maps) {
+        maps->assign(pairs.size(), {});
+        for (size_t i = 0; i < ap.size(); i++)
+            (*maps)[order[i]].assign(all.begin() + i * np, all.begin() + (i + 1) * np);
+    }
+    std::vector<std::vector<double>> out(ng);
+    for (int g = 0; g < ng; g++) out[g].assign(depth.begin() + g * np, depth.begin() + (g + 1) * np);
+    return out;
+}
+
 // ---- refinement and 3-D output ----
 // The reference's names and argument meaning; cv::Mat becomes ImageView (u8)
 // or a dense W*H std::vector<double>.  Pixels a routine does not write keep

@@ -164,8 +164,8 @@ int check_sgm(Ctx* c, const sva_sgm_params* p, int W, int H) {
 // kernel serves 1-D steps (dir_y = 0); array pairs on 2-D steps always use the
 // materialised cost volume (cost2 + sgm_paths).
 bool use_fused(const Ctx* c, const sva_sgm_params* p, int W, int H) {
-    const bool want = c->path_kernel == SVA_PATH_KERNEL_FUSED ||
-                      (c->path_kernel == SVA_PATH_KERNEL_AUTO && p->D == 256);
+    // AUTO = the cost-volume route for every D
+    const bool want = c->path_kernel == SVA_PATH_KERNEL_FUSED;
     return want && p->dir_y == 0 && fused_fits(W, H, p->D, p->dmin);
 }
 

@@ -200,6 +200,27 @@ static void gpu_tests() {
     const int pc = (H / 2) * W + W / 2;
     CHECK(nv[pc] == 2 && z[pc] == (st.baseline * cams[12].f) / ((double)d0 * cams[12].pixel_size));
 
+    // multi-GPU engine (here one device, two streams): the TO_CENTER_SMALL
+    // frame equals per-pair matching on one context + fuseDepth
+    {
+        MultiEngine me({0}, 2);
+        auto cpairs = getCameraPairs(cams, TO_CENTER_SMALL);
+        std::vector<std::vector<uint16_t>> mm;
+        auto fused = computeArrayDepth(me, views, cams, cpairs, q, 0.05, &mm);
+        CHECK(fused.size() == 1 && mm.size() == cpairs.size());
+        std::vector<std::vector<uint16_t>> single;
+        std::vector<double> bl;
+        bool same = true;
+        for (size_t i = 0; i < cpairs.size(); i++) {
+            PairStep s = pairStep(cams[cpairs[i][0]], cams[cpairs[i][1]]);
+            single.push_back(computeDisparityPair(eng, views[cpairs[i][0]], views[cpairs[i][1]], s, q));
+            bl.push_back(s.baseline);
+            same = same && single.back() == mm[i];
+        }
+        CHECK(same);
+        CHECK(fuseDepth(eng, single, W, H, bl, cams[12].f, cams[12].pixel_size) == fused[0]);
+    }
+
     // refinement: img(x) = centre(x - dd - 2) => refined disparity dd + 2 (functions.cpp:11-48)
     const int dd = 6;
     std::vector<uint8_t> other(W * H, 0), dispc(W * H, dd), fmask(W * H, 0);

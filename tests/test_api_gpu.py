@@ -123,9 +123,15 @@ def test_reserve_timing_and_errors(ctx, sva):
         ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
     assert ctx.kernel_time("cost") == (0.0, 0)
     assert ctx.kernel_time("sgm_fused")[1] == 1 and ctx.kernel_time("sgm_paths")[1] == 0
-    # AUTO (the default) picks the fused kernel for D = 256 only
+    # AUTO (the default) is the cost-volume route at every D, D = 256 included
     L2, R2, _ = synth.stereo_pair(64, 320, 256, 0, -1, seed=3)
     ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    ctx.disparity_sgm(L2, R2, sva.default_params(D=256))
+    ctx.set_timing(False)
+    assert ctx.kernel_time("cost")[1] == 1 and ctx.kernel_time("sgm_fused") == (0.0, 0)
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_FUSED)
     ctx.reset_timing()
     ctx.set_timing(True)
     ctx.disparity_sgm(L2, R2, sva.default_params(D=256))
@@ -145,7 +151,9 @@ def test_reserve_timing_and_errors(ctx, sva):
     ctx.reset_timing()
     ctx.set_timing(sva.SVA_TIMING_PATHS)
     ctx.disparity_sgm(L, R, sva.default_params(D=128))
-    ctx.disparity_sgm(L2, R2, sva.default_params(D=256))      # AUTO: fused
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_FUSED)
+    ctx.disparity_sgm(L2, R2, sva.default_params(D=256))
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
     ctx.set_timing(sva.SVA_TIMING_OFF)
     assert ctx.kernel_time("sgm_paths")[1] == 1 and ctx.kernel_time("sgm_fused")[1] == 1
     for name in ("census", "cost", "wta", "wta_h"):

@@ -159,13 +159,14 @@ def test_fused_pipeline_lr_check(fused_ctx, sva, oracle, D, dir, dmin):
     assert_sub_close(sub, oracle.lr_sub(exp, osub, 0xFFFF))
 
 
+@pytest.mark.parametrize("kern", ["auto", "fused"])
 @pytest.mark.parametrize("dir", [-1, 1])
-def test_auto_d256_lr_check(ctx, sva, oracle, dir):
-    """A context left on SVA_PATH_KERNEL_AUTO takes the fused route at D=256
-    (DESIGN.md §4.5), L/R check included."""
+def test_d256_lr_check_both_routes(ctx, sva, oracle, dir, kern):
+    """D = 256 with the L/R check on the AUTO route (the cost volume, DESIGN.md
+    §4.5) and on the fused route."""
     W, H, D, dmin = 300, 40, 256, 2
     L, R, _ = synth.stereo_pair(H, W, D, dmin, dir, seed=31, stripes=6, step=9)
-    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO if kern == "auto" else sva.SVA_PATH_KERNEL_FUSED)
     p = sva.default_params(D=D, dmin=dmin, dir=dir, lr_check=1, lr_max_diff=1, subpixel=1)
     disp, sub = ctx.disparity_sgm(L, R, p)
     dl, osub = oracle.sgm(L, R, D, dmin, dir, subpixel=True, threads=8)

@@ -235,12 +235,12 @@ def test_full_size_4k_d256_properties(ctx, sva):
     R[:, : W - d0] = L[:, d0:]
     R[:, W - d0:] = synth.texture(H, d0, 4)
     p = sva.default_params(D=D, dir=-1, subpixel=1)
-    a, sa = ctx.disparity_sgm(L, R, p)          # default AUTO: the fused kernel at D = 256
+    a, sa = ctx.disparity_sgm(L, R, p)          # default AUTO: the cost-volume route
     b, _ = ctx.disparity_sgm(L, R, p)
     assert np.array_equal(a, b)
     assert (a[8:-8, d0 + 64: W - 64] == d0).all()
     # the two path kernels agree on every disparity and sub-pixel value
-    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_COST_VOLUME)
+    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_FUSED)
     try:
         c, sc = ctx.disparity_sgm(L, R, p)
     finally:
