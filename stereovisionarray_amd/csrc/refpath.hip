@@ -609,9 +609,15 @@ __global__ __launch_bounds__(256) void ref_plane2_kernel(
 constexpr int P3_ROWS = 32;                          // 4 waves x 8 rows
 constexpr int P3_RW_MAX = 63 + 2 * PT_MAXK;          // region columns
 constexpr int P3_RS = 100;                           // R column stride: 25 dwords (odd)
-constexpr int P3_OU_BYTES = 36 * 1024;
-constexpr int P3_WORDS = 4096;                       // offset bitmap: 128K bits (4K diagonals)
-constexpr int P3_MAX_OUT = 1024;                     // outer offsets
+#ifndef SVA_P3_OU_KB
+#define SVA_P3_OU_KB 24
+#endif
+#ifndef SVA_P3_WORDS
+#define SVA_P3_WORDS 1024
+#endif
+constexpr int P3_OU_BYTES = SVA_P3_OU_KB * 1024;     // staged O chunk
+constexpr int P3_WORDS = SVA_P3_WORDS;               // offset bitmap per pass: 32K bits
+constexpr int P3_MAX_OUT = 1024;                     // outer offsets per pass
 
 // Interval [lo, lo + len) of inner offsets d_in on a pixel's line at outer
 // offset d_out; the candidate index there is i = d_in + ib0.
@@ -658,8 +664,11 @@ __device__ __forceinline__ void line_interval(int po, int pa, int pn, bool mi, b
     }
 }
 
+#ifndef SVA_P3_MINB
+#define SVA_P3_MINB 3
+#endif
 template <int K>
-__global__ __launch_bounds__(256) void ref_plane3_kernel(
+__global__ __launch_bounds__(256, SVA_P3_MINB) void ref_plane3_kernel(
     const uint8_t* __restrict__ ref, const uint8_t* __restrict__ other, int W, int H, size_t pitch,
     const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
     const uint8_t* __restrict__ valid_in, uint8_t* __restrict__ disp_u8,
@@ -677,8 +686,8 @@ __global__ __launch_bounds__(256) void ref_plane3_kernel(
     __shared__ __attribute__((aligned(16))) uint8_t OUT[P3_OU_BYTES];
     __shared__ short omn[P3_MAX_OUT], omx[P3_MAX_OUT];
     __shared__ int box[6];   // dx_lo, dx_hi, dy_lo, dy_hi, #High pixels, #pixels
+    __shared__ unsigned short uniq[P3_ROWS * 64];   // pixels with a distinct relative line
     __shared__ int nuniq;
-    unsigned short* uniq = reinterpret_cast<unsigned short*>(OUT);   // before OUT is staged
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     const int tx0 = K + blockIdx.x * 64, ty0 = K + blockIdx.y * P3_ROWS;
@@ -753,10 +762,17 @@ __global__ __launch_bounds__(256) void ref_plane3_kernel(
     const bool cm = 2 * box[4] > box[5];     // inner axis y: High lines dominate
     const int n_in = cm ? bh : bw, n_out = cm ? bw : bh;
     const int wpo = (n_in + 31) >> 5;        // bitmap words per outer offset
-    if ((long long)wpo * n_out > P3_WORDS || n_out > P3_MAX_OUT) {
-        p3_fallback:
-        // offset box too large for the bitmap (or one outer offset's O span
-        // for the staging buffer): per-pixel waves for this tile
+    // outer offsets per bitmap pass: one pass at 1080p, ~3 for a 4K diagonal
+    const int opp = min(P3_WORDS / wpo, P3_MAX_OUT);
+    // bytes of the O rectangle staged for span_out outer x span_in inner offsets
+    auto stage_bytes = [&](int span_out, int span_in) {
+        const int cw = RW + (cm ? span_out : span_in) - 1;
+        const int ch = 24 + (cm ? span_in : span_out) - 1 + 4 * (ND2 + 1);
+        return cw * ((((ch + 3) >> 2) | 1) << 2);
+    };
+    if (opp < 1 || stage_bytes(1, 1) > P3_OU_BYTES) {
+        // one outer offset's bitmap row or O column does not fit: per-pixel
+        // waves for this tile
         for (int pi = wv; pi < 64 * P3_ROWS; pi += 4) {
             const int x = tx0 + (pi & 63), y = ty0 + (pi >> 6);
             if (x >= W - K || y >= H - K) continue;
@@ -767,8 +783,6 @@ __global__ __launch_bounds__(256) void ref_plane3_kernel(
         }
         return;
     }
-    const int nwords = wpo * n_out;
-    for (int i = t; i < nwords; i += 256) bits[i] = 0;
     if (t == 0) nuniq = 0;
     __syncthreads();
     // Bresenham is translation-invariant: pixels whose endpoints, relative
@@ -796,58 +810,10 @@ __global__ __launch_bounds__(256) void ref_plane3_kernel(
         }
     }
     __syncthreads();
-    // one thread per distinct line, walking it incrementally (the minor
-    // offset of point i advances by at most one per step since a <= b)
-    const int bstride = wpo * 32;
-    for (int q = t; q < nuniq; q += 256) {
-        const int pl = uniq[q], x = tx0 + (pl & 63), y = ty0 + (pl >> 6);
-        const int4 e = ends[(size_t)y * W + x];
-        const Line L = make_line(e.x, e.y, e.z, e.w);
-        int mnr = L.b > 0 ? (L.major - 1) / L.b : 0;
-        int rem = L.b > 0 ? (L.major - 1) - mnr * L.b : 0;
-        const int bx0 = L.x0 - x - dxlo, by0 = L.y0 - y - dylo;
-        for (int i = 0; i < L.n; i++) {
-            const int off = L.step * mnr;
-            const int rx = L.high ? bx0 + off : bx0 + i;
-            const int ry = L.high ? by0 + i : by0 + off;
-            const int b = cm ? rx * bstride + ry : ry * bstride + rx;
-            atomicOr(&bits[b >> 5], 1u << (b & 31));
-            rem += L.a;
-            if (rem >= L.b) {
-                rem -= L.b;
-                mnr++;
-            }
-        }
-    }
-    __syncthreads();
-    // Per outer offset, the first and last inner offset with a plane.  The
-    // planes are staged in chunks of consecutive outer offsets whose O
-    // rectangle fits OUT (one chunk for Low/High pairs at 1080p; diagonal
-    // pairs, whose offset box is a thin diagonal band, take a few); an outer
-    // offset whose inner span alone does not fit is split into windows.
-    auto stage_bytes = [&](int span_out, int span_in) {
-        const int cw = RW + (cm ? span_out : span_in) - 1;
-        const int ch = 24 + (cm ? span_in : span_out) - 1 + 4 * (ND2 + 1);
-        return cw * ((((ch + 3) >> 2) | 1) << 2);
-    };
-    for (int o = t; o < n_out; o += 256) {
-        int mn = 0x7fff, mx = -1;
-        for (int wc = 0; wc < wpo; wc++) {
-            const unsigned m = bits[o * wpo + wc];
-            if (m) {
-                mn = min(mn, wc * 32 + __builtin_ctz(m));
-                mx = max(mx, wc * 32 + 31 - __builtin_clz(m));
-            }
-        }
-        omn[o] = (short)mn;
-        omx[o] = (short)mx;
-    }
-    if (stage_bytes(1, 1) > P3_OU_BYTES) goto p3_fallback;   // uniform (k, box)
-    // widest inner window of a single outer offset
+    // widest inner window of a single outer offset (uniform)
     int iwmax = 1;
     for (int step = 1 << 12; step; step >>= 1)
         if (iwmax + step <= n_in && stage_bytes(1, iwmax + step) <= P3_OU_BYTES) iwmax += step;
-    __syncthreads();
 
     // R dwords of this lane's two region columns, rows r0 .. r0 + 4*ND2 - 1
     const int ca = lane, cb = min(lane + 64, RW - 1);
@@ -918,84 +884,149 @@ __global__ __launch_bounds__(256) void ref_plane3_kernel(
     }
     const int in_lo = cm ? dylo : dxlo, out_lo = cm ? dxlo : dylo;
     const int src = ((lane + W2 - 1) & 63) << 2;
-    for (int o0 = 0, wst = -1;;) {           // wst >= 0: outer offset o0 continues there
-        if (wst < 0) {
-            while (o0 < n_out && __builtin_amdgcn_readfirstlane(omn[o0] > omx[o0])) o0++;
-            if (o0 >= n_out) break;
-        }
-        int o1 = o0 + 1;
-        int ilo = __builtin_amdgcn_readfirstlane(omn[o0]);
-        int ihi = __builtin_amdgcn_readfirstlane(omx[o0]);
-        if (wst >= 0 || ihi - ilo + 1 > iwmax) {
-            // one outer offset, inner window [ilo, ihi]
-            const int end = ihi;
-            ilo = wst >= 0 ? wst : ilo;
-            ihi = min(end, ilo + iwmax - 1);
-            wst = ihi < end ? ihi + 1 : -1;
-        } else {
-            // grow the chunk [o0, o1) while its O rectangle fits
-            for (; o1 < n_out; o1++) {
-                const int a = __builtin_amdgcn_readfirstlane(omn[o1]);
-                const int b = __builtin_amdgcn_readfirstlane(omx[o1]);
-                const int nl = a <= b ? min(ilo, a) : ilo, nh = a <= b ? max(ihi, b) : ihi;
-                if (stage_bytes(o1 + 1 - o0, nh - nl + 1) > P3_OU_BYTES) break;
-                ilo = nl;
-                ihi = nh;
+    const int bstride = wpo * 32;
+    for (int oa = 0; oa < n_out; oa += opp) {
+        const int nl = min(n_out - oa, opp);    // outer offsets of this bitmap pass
+        __syncthreads();                     // the previous pass's planes are done
+        for (int i = t; i < wpo * nl; i += 256) bits[i] = 0;
+        __syncthreads();
+        // one thread per distinct line, walking it incrementally (the minor
+        // offset of point i advances by at most one per step since a <= b);
+        // consecutive points mostly fall in one bitmap word (runs along the
+        // major axis), so they are gathered in a mask: one atomic per word
+        for (int q = t; q < nuniq; q += 256) {
+            const int pl = uniq[q], x = tx0 + (pl & 63), y = ty0 + (pl >> 6);
+            const int4 e = ends[(size_t)y * W + x];
+            const Line L = make_line(e.x, e.y, e.z, e.w);
+            int mnr = L.b > 0 ? (L.major - 1) / L.b : 0;
+            int rem = L.b > 0 ? (L.major - 1) - mnr * L.b : 0;
+            const int bx0 = L.x0 - x - dxlo, by0 = L.y0 - y - dylo;
+            int cur = -1;
+            unsigned msk = 0;
+            for (int i = 0; i < L.n; i++) {
+                const int off = L.step * mnr;
+                const int rx = L.high ? bx0 + off : bx0 + i;
+                const int ry = L.high ? by0 + i : by0 + off;
+                const int ro = (cm ? rx : ry) - oa;
+                if ((unsigned)ro < (unsigned)nl) {
+                    const int b = ro * bstride + (cm ? ry : rx);
+                    if ((b >> 5) != cur) {
+                        if (msk) atomicOr(&bits[cur], msk);
+                        cur = b >> 5;
+                        msk = 0;
+                    }
+                    msk |= 1u << (b & 31);
+                }
+                rem += L.a;
+                if (rem >= L.b) {
+                    rem -= L.b;
+                    mnr++;
+                }
             }
-        }
-        // O over the chunk: columns rx0 + dxb + [0, ouw), rows ry0 + dyb +
-        // [0, ouh) (every dword a plane reads), column stride os (odd dwords)
-        const int dxb = cm ? out_lo + o0 : in_lo + ilo, dyb = cm ? in_lo + ilo : out_lo + o0;
-        const int ouw = RW + (cm ? o1 - o0 : ihi - ilo + 1) - 1;
-        const int ouh = 24 + (cm ? ihi - ilo + 1 : o1 - o0) - 1 + 4 * (ND2 + 1);
-        const int os = ((((ouh + 3) >> 2) | 1) << 2);
-        __syncthreads();                     // the previous chunk's planes are done
-        {
-            const int ox0 = rx0 + dxb, oy0 = ry0 + dyb;
-            for (int i = t; i < ouw * ouh; i += 256) {
-                const int v = i / ouw, u = i - v * ouw;
-                const int gx = ox0 + u, gy = oy0 + v;
-                OUT[u * os + v] = (gx >= 0 && gx < W && gy >= 0 && gy < H)
-                                      ? other[(size_t)gy * pitch + gx] : 0;
-            }
+            if (msk) atomicOr(&bits[cur], msk);
         }
         __syncthreads();
-        for (int ot = o0; ot < o1; ot++) {
-            const int d_out = out_lo + ot;
-            const int wlo = max(ilo, __builtin_amdgcn_readfirstlane(omn[ot]));
-            const int whi = min(ihi, __builtin_amdgcn_readfirstlane(omx[ot]));
-            if (wlo > whi) continue;
+        // Per outer offset, the first and last inner offset with a plane.  The
+        // planes are staged in chunks of consecutive outer offsets whose O
+        // rectangle fits OUT (one chunk for Low/High pairs at 1080p; diagonal
+        // pairs, whose offset box is a thin diagonal band, take a few); an
+        // outer offset whose inner span alone does not fit is split into
+        // windows.
+        for (int o = t; o < nl; o += 256) {
+            int mn = 0x7fff, mx = -1;
+            for (int wc = 0; wc < wpo; wc++) {
+                const unsigned m = bits[o * wpo + wc];
+                if (m) {
+                    mn = min(mn, wc * 32 + __builtin_ctz(m));
+                    mx = max(mx, wc * 32 + 31 - __builtin_clz(m));
+                }
+            }
+            omn[o] = (short)mn;
+            omx[o] = (short)mx;
+        }
+        __syncthreads();
+        for (int o0 = 0, wst = -1;;) {           // wst >= 0: outer offset o0 continues there
+            if (wst < 0) {
+                while (o0 < nl && __builtin_amdgcn_readfirstlane(omn[o0] > omx[o0])) o0++;
+                if (o0 >= nl) break;
+            }
+            int o1 = o0 + 1;
+            int ilo = __builtin_amdgcn_readfirstlane(omn[o0]);
+            int ihi = __builtin_amdgcn_readfirstlane(omx[o0]);
+            if (wst >= 0 || ihi - ilo + 1 > iwmax) {
+                // one outer offset, inner window [ilo, ihi]
+                const int end = ihi;
+                ilo = wst >= 0 ? wst : ilo;
+                ihi = min(end, ilo + iwmax - 1);
+                wst = ihi < end ? ihi + 1 : -1;
+            } else {
+                // grow the chunk [o0, o1) while its O rectangle fits
+                for (; o1 < nl; o1++) {
+                    const int a = __builtin_amdgcn_readfirstlane(omn[o1]);
+                    const int b = __builtin_amdgcn_readfirstlane(omx[o1]);
+                    const int gl = a <= b ? min(ilo, a) : ilo, gh = a <= b ? max(ihi, b) : ihi;
+                    if (stage_bytes(o1 + 1 - o0, gh - gl + 1) > P3_OU_BYTES) break;
+                    ilo = gl;
+                    ihi = gh;
+                }
+            }
+            // O over the chunk: columns rx0 + dxb + [0, ouw), rows ry0 + dyb +
+            // [0, ouh) (every dword a plane reads), column stride os (odd dwords)
+            const int dxb = cm ? out_lo + oa + o0 : in_lo + ilo;
+            const int dyb = cm ? in_lo + ilo : out_lo + oa + o0;
+            const int ouw = RW + (cm ? o1 - o0 : ihi - ilo + 1) - 1;
+            const int ouh = 24 + (cm ? ihi - ilo + 1 : o1 - o0) - 1 + 4 * (ND2 + 1);
+            const int os = ((((ouh + 3) >> 2) | 1) << 2);
+            __syncthreads();                     // the previous chunk's planes are done
+            {
+                const int ox0 = rx0 + dxb, oy0 = ry0 + dyb;
+                for (int i = t; i < ouw * ouh; i += 256) {
+                    const int v = i / ouw, u = i - v * ouw;
+                    const int gx = ox0 + u, gy = oy0 + v;
+                    OUT[u * os + v] = (gx >= 0 && gx < W && gy >= 0 && gy < H)
+                                          ? other[(size_t)gy * pitch + gx] : 0;
+                }
+            }
+            __syncthreads();
+            for (int ot = o0; ot < o1; ot++) {
+                const int d_out = out_lo + oa + ot;
+                const int wlo = max(ilo, __builtin_amdgcn_readfirstlane(omn[ot]));
+                const int whi = min(ihi, __builtin_amdgcn_readfirstlane(omx[ot]));
+                if (wlo > whi) continue;
 #pragma unroll
-            for (int j = 0; j < 8; j++)
-                line_interval(po[j], pa[j], pn[j], high[j] == cm, neg[j], d_out, lo[j], len[j],
-                              ib0[j]);
-            for (int wc = wlo >> 5; wc <= (whi >> 5); wc++) {
-                unsigned m = (unsigned)__builtin_amdgcn_readfirstlane((int)bits[ot * wpo + wc]);
-                if (wc == (wlo >> 5)) m &= ~0u << (wlo & 31);            // window edges
-                if (wc == (whi >> 5)) m &= ~0u >> (31 - (whi & 31));
-                while (m) {
-                    const int d_in = in_lo + wc * 32 + __builtin_ctz(m);
-                    m &= m - 1;
-                    const int ddx = cm ? d_out : d_in, ddy = cm ? d_in : d_out;
-                    const int ob = (ddx - dxb) * os + (ddy - dyb) + r0;
-                    unsigned csA[8], csB[8];
-                    colsums(RA, reA0, reA1, ob + ca * os, csA);
-                    colsums(RB, reB0, reB1, ob + cb * os, csB);
+                for (int j = 0; j < 8; j++)
+                    line_interval(po[j], pa[j], pn[j], high[j] == cm, neg[j], d_out, lo[j],
+                                  len[j], ib0[j]);
+                for (int wc = wlo >> 5; wc <= (whi >> 5); wc++) {
+                    unsigned m =
+                        (unsigned)__builtin_amdgcn_readfirstlane((int)bits[ot * wpo + wc]);
+                    if (wc == (wlo >> 5)) m &= ~0u << (wlo & 31);            // window edges
+                    if (wc == (whi >> 5)) m &= ~0u >> (31 - (whi & 31));
+                    while (m) {
+                        const int d_in = in_lo + wc * 32 + __builtin_ctz(m);
+                        m &= m - 1;
+                        const int ddx = cm ? d_out : d_in, ddy = cm ? d_in : d_out;
+                        const int ob = (ddx - dxb) * os + (ddy - dyb) + r0;
+                        unsigned csA[8], csB[8];
+                        colsums(RA, reA0, reA1, ob + ca * os, csA);
+                        colsums(RB, reB0, reB1, ob + cb * os, csB);
 #pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        const unsigned Pa = scan64_dpp(csA[j]), Pb = scan64_dpp(csB[j]);
-                        const unsigned ta = (unsigned)__builtin_amdgcn_readlane((int)Pa, 63);
-                        const unsigned V = lane < W2 - 1 ? Pb + ta : Pa;
-                        const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)V);
-                        const unsigned sad = hi - Pa + csA[j];
-                        const unsigned key = (sad << 12) | (unsigned)(d_in + ib0[j]);
-                        const bool on = (unsigned)(d_in - lo[j]) < (unsigned)len[j];
-                        best[j] = on ? min(best[j], key) : best[j];
+                        for (int j = 0; j < 8; j++) {
+                            const unsigned Pa = scan64_dpp(csA[j]), Pb = scan64_dpp(csB[j]);
+                            const unsigned ta = (unsigned)__builtin_amdgcn_readlane((int)Pa, 63);
+                            const unsigned V = lane < W2 - 1 ? Pb + ta : Pa;
+                            const unsigned hi =
+                                (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)V);
+                            const unsigned sad = hi - Pa + csA[j];
+                            const unsigned key = (sad << 12) | (unsigned)(d_in + ib0[j]);
+                            const bool on = (unsigned)(d_in - lo[j]) < (unsigned)len[j];
+                            best[j] = on ? min(best[j], key) : best[j];
+                        }
                     }
                 }
             }
+            if (wst < 0) o0 = o1;
         }
-        if (wst < 0) o0 = o1;
     }
 #pragma unroll
     for (int j = 0; j < 8; j++) {
