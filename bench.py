@@ -482,10 +482,36 @@ def run_array(a, wl, world, rank, local, dev):
         cstreams.append(s_)
 
     # compute-only steps (exchange_report) fuse a stand-in buffer of the full size
+    # multi: the exchange runs (N > 1, or a 1-rank RCCL group with --rehearse-rccl)
+    multi = world > 1 or a.rehearse_rccl
     stand_in = torch.zeros((n_units, H, W), dtype=torch.int16, device=dev) \
-        if world > 1 and rank == 0 else None
+        if multi and rank == 0 else None
+    # N > 1 over RCCL: step i computes into map buffer i % 2 while the gather
+    # of step i - 1 and rank 0's fusion of it run on a comm stream (fused by a
+    # context bound to that stream), as in main()
+    overlap = multi and a.dist_backend == "nccl" and not a.no_overlap
+    disps = [disp] + ([torch.zeros_like(disp)] if overlap else [])
+    comm = torch.cuda.Stream(dev) if overlap else None
+    fctx = None
+    if overlap and rank == 0:
+        fctx = sva.Context(local)
+        fctx.set_stream(comm.cuda_stream)
+    pending = [None] * len(disps)        # buffer -> event after its gather (+ fusion)
+    it = [0]
+
+    def fuse(c, allm):
+        for g, (i, o, n, bases) in enumerate(groups):
+            c.fuse_depth_d(allm[o].data_ptr(), n, W, H, bases, ARRAY_F, ARRAY_PS, 0xFFFF,
+                           depth[g].data_ptr(), nvalid[g].data_ptr())
+        maps["all"] = allm
 
     def step(exchange=True):
+        b = it[0] % len(disps)
+        it[0] += 1
+        dsp = disps[b]
+        if pending[b] is not None:       # this buffer's previous gather has read it
+            stream.wait_event(pending[b])
+            pending[b] = None
         if len(ctxs) > 1:                # the previous step's fusion has read disp
             go = torch.cuda.Event()
             go.record(stream)
@@ -493,32 +519,42 @@ def run_array(a, wl, world, rank, local, dev):
                 s_.wait_event(go)
         for jb, (L, R, p) in enumerate(jobs):
             ctxs[jb % len(ctxs)].disparity_sgm_d(L.data_ptr(), R.data_ptr(), W, H, W, p,
-                                                 disp[jb].data_ptr())
+                                                 dsp[jb].data_ptr())
         for s_ in cstreams[1:]:
             done_ = torch.cuda.Event()
             done_.record(s_)
             stream.wait_event(done_)
-        if world > 1 and not exchange:
+        if multi and exchange and overlap:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            with torch.cuda.stream(comm):
+                comm.wait_event(ev)
+                dsp.record_stream(comm)
+                allm = sdist.gather_maps(dsp, n_units, dst=0)
+                if rank == 0:
+                    fuse(fctx, allm)
+                e2 = torch.cuda.Event()
+                e2.record(comm)
+                pending[b] = e2
+            return
+        if multi and not exchange:
             allm = stand_in
-        elif world > 1:
+        elif multi:
             if a.dist_backend == "nccl":
-                allm = sdist.gather_maps(disp, n_units, dst=0)
+                allm = sdist.gather_maps(dsp, n_units, dst=0)
             else:
-                allm = sdist.gather_maps(disp.cpu(), n_units, dst=0)
+                allm = sdist.gather_maps(dsp.cpu(), n_units, dst=0)
                 allm = allm.to(dev) if allm is not None else None
         else:
-            allm = disp
+            allm = dsp
         if rank == 0:
-            for g, (i, o, n, bases) in enumerate(groups):
-                ctx.fuse_depth_d(allm[o].data_ptr(), n, W, H, bases, ARRAY_F, ARRAY_PS, 0xFFFF,
-                                 depth[g].data_ptr(), nvalid[g].data_ptr())
-            maps["all"] = allm
+            fuse(ctx, allm)
 
     elapsed = timed(a, step, world, dev, ctxs)
     kernels = breakdown(a, step, world, ctxs, kernel_table(ctxs))
     value = n_units * W * H * D * a.steps / elapsed / 1e6
     exchange = None
-    if world > 1:
+    if multi:
         def recompute(u):
             i, j = pairs[u]
             sx, sy, _ = synth.pair_step(grid[i], grid[j])
@@ -528,8 +564,8 @@ def run_array(a, wl, world, rank, local, dev):
             ctx.disparity_sgm_d(Ld.data_ptr(), Rd.data_ptr(), W, H, W,
                                 sva.default_params(D=D, dmin=0, dir=sx, dir_y=sy), m.data_ptr())
             return m
-        exchange = exchange_report(a, step, world, rank, dev, ctxs, disp, n_units,
-                                   elapsed / a.steps * 1e3, recompute)
+        exchange = exchange_report(a, step, world, rank, dev, ctxs, disps[(it[0] - 1) % len(disps)],
+                                   n_units, elapsed / a.steps * 1e3, recompute)
         step()                           # the compute-only steps fused the stand-in
         torch.cuda.synchronize()
     out = None
@@ -565,7 +601,8 @@ def run_array(a, wl, world, rank, local, dev):
                                    "Mode S along each pair's baseline step, RCCL gather, "
                                    "per-camera median fusion on rank 0",
                        "W": W, "H": H, "D": D, "P1": 10, "P2": 120, "pairs": n_units,
-                       "parallelism": f"pairs sharded over {world} rank(s), gather to rank 0",
+                       "parallelism": f"pairs sharded over {world} rank(s), gather to rank 0"
+                                      + (" overlapped with the next step" if overlap else ""),
                        "streams_per_rank": len(ctxs)},
             "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
             "fused_maps_per_s": round(len(groups) * a.steps / elapsed, 2),
@@ -578,9 +615,9 @@ def run_array(a, wl, world, rank, local, dev):
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(W, H, D, a.cpu_threads)
         print(json.dumps(out), flush=True)
-    for c in ctxs:
+    for c in ctxs + ([fctx] if fctx is not None else []):
         c.close()
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
     if exchange is not None and not exchange["ok"]:
         raise SystemExit("multi-rank exchange check failed: " + json.dumps(exchange))
