@@ -266,13 +266,30 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
     int x0, y0;
     if (ry == 0) { y0 = line; x0 = rx > 0 ? 0 : W - 1; }
     else { y0 = ry > 0 ? 0 : H - 1; x0 = line; }
-    Cursor<DIAG> cc;
+    Cursor<false> cc;
     cc.x = x0;
     cc.off = ((unsigned)y0 * (unsigned)W + (unsigned)x0) * (unsigned)D + (unsigned)(k * DPL);
     // Prefetch cursor: runs PF steps ahead and may run past the line's end;
     // those loads land in-range garbage or, past the volume, the buffer range
     // check returns 0 -- never consumed either way.
-    Cursor<DIAG> pc = cc;
+    Cursor<false> pc = cc;
+    // Diagonal lines wrap without per-step x tracking.  Line l visits
+    // x = (l + rx*t) mod W and wraps between pixels s and s+1 when s + 1 =
+    // W - l (rx = +1) or l + 1 (rx = -1), then every W steps: tw* hold each
+    // lane's next wrap pixel for the compute and prefetch cursors.  A wave's
+    // four lines are consecutive, so their wraps fall in one 4-step window per
+    // period that starts at the wave-uniform pixel T*; only window steps pay
+    // per-lane work (one uniform branch), the others a scalar compare.  (The
+    // x tracking had cost ~29 VALU per diagonal step: 78 against 49 for a
+    // vertical step.)  Images narrower than 4 columns check every step.
+    int twc = 0, twp = 0, Tc = 0, Tp = 0;
+    if constexpr (DIAG) {
+        const int j = (int)((threadIdx.x >> 4) & 3);          // row of the line in its wave
+        const int l0 = __builtin_amdgcn_readfirstlane(line - j);
+        twc = twp = rx > 0 ? W - line : line + 1;
+        Tc = Tp = rx > 0 ? W - l0 - 3 : l0 + 1;
+    }
+    const bool narrow = W < 4;
 
     unsigned A[NP];
 #pragma unroll
@@ -288,7 +305,18 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
         } else {
             ring[p] = bload<NW>(rC, pc.off);
         }
-        pc.advance(rx, stride, W, WD);
+        pc.off += stride;
+        if constexpr (DIAG) {   // the advance past pixel PF-1 is checked by step 0
+            if (p < PF - 1) {
+                const bool w = p + 1 == twp;
+                const unsigned fixed = rx > 0 ? pc.off - WD : pc.off + WD;
+                pc.off = w ? fixed : pc.off;
+                twp = w ? twp + W : twp;
+            }
+        }
+    }
+    if constexpr (DIAG) {       // prefetch windows the prologue has fully handled
+        while (Tp + 3 < PF) Tp += W;
     }
 
     // One step consumes ring slot p in place (loaded PF steps ago) and only
@@ -314,11 +342,35 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
         } else {
             bstore<NW, VAR>(rL, cc.off, ow);
         }
-        const bool wrapped = cc.advance(rx, stride, W, WD);
-        if constexpr (DIAG) {   // restart where x wraps: selects, no divergent branch
+        cc.off += stride;
+        if constexpr (DIAG) {
+            // One uniform branch, taken only on the steps of a wrap window of
+            // either cursor: the compute cursor restarts where x wraps (L = C),
+            // and the prefetch cursor's previous advance (past pixel
+            // ts + PF - 1) is corrected before its next load.
+            const int ec = ts + 1 - Tc;
+            const int ep = ts + PF - Tp;
+            const bool cev = narrow || (unsigned)ec < 4u;
+            const bool pev = refill && (narrow || (unsigned)ep < 4u);
+            if (cev || pev) {
+                if (cev) {
+                    const bool wrapped = ts + 1 == twc;
+                    const unsigned fixed = rx > 0 ? cc.off - WD : cc.off + WD;
+                    cc.off = wrapped ? fixed : cc.off;
+                    twc = wrapped ? twc + W : twc;
 #pragma unroll
-            for (int j = 0; j < NP; j++) A[j] = wrapped ? 0u : A[j];
-            m = wrapped ? 0u : m;
+                    for (int j = 0; j < NP; j++) A[j] = wrapped ? 0u : A[j];
+                    m = wrapped ? 0u : m;
+                    if (ec == 3) Tc += W;
+                }
+                if (pev) {
+                    const bool wrapped = ts + PF == twp;
+                    const unsigned fixed = rx > 0 ? pc.off - WD : pc.off + WD;
+                    pc.off = wrapped ? fixed : pc.off;
+                    twp = wrapped ? twp + W : twp;
+                    if (ep == 3) Tp += W;
+                }
+            }
         }
         if (refill) {
             __builtin_amdgcn_sched_barrier(0);
@@ -328,7 +380,7 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
             } else {
                 ring[p] = bload<NW>(rC, pc.off);
             }
-            pc.advance(rx, stride, W, WD);
+            pc.off += stride;                // wrap corrected by the next step
             __builtin_amdgcn_sched_barrier(0);
         }
     };

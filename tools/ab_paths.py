@@ -144,7 +144,8 @@ def main():
                 t = L8 if a.entry == "ckpt" else disp
                 outs.append(torch.sum(t.view(torch.int64) if t.dtype == torch.uint8 else
                                       t.to(torch.int64)).item())
-            assert len(set(outs)) == 1, outs
+            if not os.environ.get("AB_NOCHECK"):     # ablation builds compute other values
+                assert len(set(outs)) == 1, outs
         if a.entry == "paths" and it == 0:
             # every variant must produce the same volumes
             outs = []
