@@ -139,6 +139,18 @@ struct Cursor {
     }
 };
 
+// Three-input packed u16 min through gfx950's v_pk_minimum3_f16.  Exact for
+// this kernel's operands: non-negative integers below 1024 (L <= 254, m + P2
+// <= 447), i.e. f16 zero/denormal bit patterns, which order like the
+// integers (kernels keep f16 denormals: .amdhsa_float_denorm_mode_16_64 3).
+// INF (0x7fff, a NaN pattern) never reaches it: the row-end neighbour only
+// enters through the integer v_pk_min_u16 with a real neighbour.
+__device__ __forceinline__ unsigned min3_u16x2(unsigned a, unsigned b, unsigned c) {
+    unsigned r;
+    asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // One recurrence step for the lane's DPL disparities.  State A = L(q, .)
 // (unnormalised u16 pairs), m = min_k L(q, k) broadcast over the row.
 //   u      = min(min(A(d-1), A(d+1)) + P1, A(d), m + P2)      (all >= m)
@@ -158,8 +170,9 @@ __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigne
 #pragma unroll
     for (int j = 1; j < NP; j++) M[j] = __builtin_amdgcn_alignbit(A[j], A[j - 1], 16);
     const unsigned Qlast = __builtin_amdgcn_alignbit(Y, A[NP - 1], 16);
-    const unsigned mP2 = m + P2;
-    const unsigned K = 0u - (m | (m << 16));
+    const unsigned m2 = m | (m << 16);
+    const unsigned mP2 = m2 + P2 * 0x10001u;
+    const unsigned K = 0u - m2;
     // Stage-major over the NP independent pairs, and a min TREE below: each
     // packed op's result is consumed one pair later, not by the next
     // instruction (gfx950 puts an s_nop between dependent VOP3P ops).
@@ -169,21 +182,29 @@ __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigne
 #pragma unroll
     for (int j = 0; j < NP; j++) t[j] = t[j] + splat2(P1);
 #pragma unroll
-    for (int j = 0; j < NP; j++) t[j] = vmin2(t[j], as_v2(A[j]));
-#pragma unroll
-    for (int j = 0; j < NP; j++) t[j] = vmin2(t[j], splat2(mP2));
-#pragma unroll
-    for (int j = 0; j < NP; j++) A[j] = add3(as_u32(t[j]), c[j], K);
+    for (int j = 0; j < NP; j++) A[j] = add3(min3_u16x2(as_u32(t[j]), A[j], mP2), c[j], K);
 #pragma unroll
     for (int w = 0; w < NW; w++) ow[w] = pack4(A[2 * w], A[2 * w + 1]);
-    u16x2 mm[NP];
+    // min over the lane's pairs: three-input mins, then the two halves
+    unsigned mm[NP];
 #pragma unroll
-    for (int j = 0; j < NP; j++) mm[j] = as_v2(A[j]);
+    for (int j = 0; j < NP; j++) mm[j] = A[j];
+    int n = NP;
 #pragma unroll
-    for (int s = 1; s < NP; s *= 2)
+    for (int it = 0; it < 4; it++) {
+        if (n > 1) {
+            int o = 0, i = 0;
 #pragma unroll
-        for (int j = 0; j + s < NP; j += 2 * s) mm[j] = vmin2(mm[j], mm[j + s]);
-    m = row_min_u32(mm[0].x < mm[0].y ? mm[0].x : mm[0].y);
+            for (int q = 0; q < 8; q++) {
+                if (i + 2 < n) { mm[o++] = min3_u16x2(mm[i], mm[i + 1], mm[i + 2]); i += 3; }
+                else if (i + 1 < n) { mm[o++] = as_u32(vmin2(as_v2(mm[i]), as_v2(mm[i + 1]))); i += 2; }
+                else if (i < n) { mm[o++] = mm[i]; i += 1; }
+            }
+            n = o;
+        }
+    }
+    const u16x2 mf = as_v2(mm[0]);
+    m = row_min_u32(mf.x < mf.y ? mf.x : mf.y);
 }
 
 // The same step on u8-packed cost words (DPL/4 dwords of 4 disparities).
