@@ -843,12 +843,18 @@ __global__ __launch_bounds__(256, SVA_P3_MINB) void ref_plane3_kernel(
         for (int q = 0; q <= ND2; q++) raw[q] = w[q];
 #pragma unroll
         for (int q = 0; q < ND2; q++) O[q] = __builtin_amdgcn_alignbyte(raw[q + 1], raw[q], sh);
+        // |o - r| summed over the first j bytes only: the other bytes of o are
+        // replaced by r's (one v_perm) so they add 0 -- cheaper than masking
+        // both operands.  Selector: bytes < j from o (4..7), the rest from r.
+        auto sad_first = [](unsigned o, unsigned r, int j, unsigned acc) -> unsigned {
+            const unsigned sel = j == 1 ? 0x03020104u : j == 2 ? 0x03020504u : 0x03060504u;
+            return __builtin_amdgcn_sad_u8(__builtin_amdgcn_perm(o, r, sel), r, acc);
+        };
         unsigned s0 = 0;
 #pragma unroll
         for (int q = 0; q < ND; q++) {
-            unsigned o = O[q], r = R[q];
-            if (ODD && q == ND - 1) { o &= 0xffffu; r &= 0xffffu; }
-            s0 = __builtin_amdgcn_sad_u8(o, r, s0);
+            if (ODD && q == ND - 1) s0 = sad_first(O[q], R[q], 2, s0);
+            else s0 = __builtin_amdgcn_sad_u8(O[q], R[q], s0);
         }
         const unsigned oe0 = entering(O, 0), oe1 = entering(O, 1);
         // X_j = sum of the j rows leaving, E_j = s0 + sum of the j rows entering
@@ -858,13 +864,8 @@ __global__ __launch_bounds__(256, SVA_P3_MINB) void ref_plane3_kernel(
         cs[4] = e4 - x4;
 #pragma unroll
         for (int j = 1; j < 4; j++) {
-            const unsigned m = (1u << (8 * j)) - 1u;
-            const unsigned xj = __builtin_amdgcn_sad_u8(O[0] & m, R[0] & m, 0u);
-            const unsigned ej = __builtin_amdgcn_sad_u8(oe0 & m, re0 & m, s0);
-            cs[j] = ej - xj;
-            const unsigned xk = __builtin_amdgcn_sad_u8(O[1] & m, R[1] & m, x4);
-            const unsigned ek = __builtin_amdgcn_sad_u8(oe1 & m, re1 & m, e4);
-            cs[4 + j] = ek - xk;
+            cs[j] = sad_first(oe0, re0, j, s0) - sad_first(O[0], R[0], j, 0u);
+            cs[4 + j] = sad_first(oe1, re1, j, e4) - sad_first(O[1], R[1], j, x4);
         }
     };
 
