@@ -202,10 +202,9 @@ __global__ __launch_bounds__(256) void ref_match_kernel(
 //      offset floor((a*i + major - 1) / b) -- keeping the minimum key over
 //      (SAD, i): the reference's first minimum (CameraStereoVision.cpp:85)
 //      whatever order the planes are visited in.
-// A tile whose offset box exceeds the bitmap falls back to match_pixel_wave.
-constexpr int PT_REG_W = 64;                 // v2 region width = TW + 2k
-constexpr int PT_MAXK = 28;                  // largest k of the plane kernels
-constexpr int PT_MAXBITS = 1 << 15;          // offset bitmap capacity
+// A tile whose offset geometry exceeds the kernel's buffers falls back to
+// match_pixel_wave.
+constexpr int PT_MAXK = 28;                  // largest k of the plane kernel
 
 // Inclusive wave64 scan in 6 DPP adds (no LDS): Hillis-Steele within each
 // 16-lane row (row_shr 1, 2, 4, 8; lanes with no source read 0), then
@@ -222,370 +221,11 @@ __device__ __forceinline__ unsigned scan64_dpp(unsigned v) {
     return v;
 }
 
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-__device__ __forceinline__ rsrc_t make_rsrc(const void* base, unsigned bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
-                                             0x00020000);
-}
-
-// ---- offset-plane algorithm, v2 (A/B reference for v3: SVA_REF_PLANE=2) --------
-// A tile of TW = 64 - 2k pixel columns x 32 rows, whose window-extended region
-// is exactly 64 columns wide (one lane per region column):
-//   * R, the staged O union and the AD planes are held column-major in LDS
-//     (byte (col, row) at col * stride + row, stride an odd number of dwords),
-//     so a lane that owns a column reads 4 rows per ds_read_b32 and the 2k-row
-//     column sum is k/2 v_sad_u8(dword, 0) byte sums.
-//   * Wave w owns output rows 8w..8w+7 and lane = output column: it turns its
-//     own column sums into SADs with a DPP scan and one ds_bpermute
-//     (SAD = P[lane + 2k - 1] - P[lane] + col[lane]) and tests membership for
-//     its own pixels, whose lines and best keys stay in registers.  No prefix
-//     table, no second pass.
-//   * Two planes per iteration: one barrier per plane instead of two.
-//   * Tiles whose O union does not fit the staging buffer read O with raw
-//     buffer loads (a valid pixel's windows lie inside the image, so the
-//     bytes a clamped or wrapped column brings in never reach its SAD).
-constexpr int P2_ROWS = 32;                           // 4 waves x 8 rows
-constexpr int P2_RS = 92;                             // R / AD column stride: 23 dwords >= 88 rows
-constexpr int P2_OU_BYTES = 24 * 1024;
-
-__device__ __forceinline__ unsigned bytes4(const uint8_t* lds, int byte_off) {
-    // 4 bytes at any byte offset of an LDS image: two aligned dwords, realigned
-    const unsigned* w = reinterpret_cast<const unsigned*>(lds) + (byte_off >> 2);
-    const unsigned sh = (unsigned)(byte_off & 3);
-    return sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
-}
-
-__device__ __forceinline__ unsigned absdiff4(unsigned o, unsigned r) {
-    // |o - r| per byte, even and odd bytes as u16 pairs: max - min
-    const u16x2 oe = as_v2(o & 0x00ff00ffu), oo = as_v2((o >> 8) & 0x00ff00ffu);
-    const u16x2 re = as_v2(r & 0x00ff00ffu), ro = as_v2((r >> 8) & 0x00ff00ffu);
-    const unsigned de = as_u32(__builtin_elementwise_max(oe, re) - vmin2(oe, re));
-    const unsigned dd = as_u32(__builtin_elementwise_max(oo, ro) - vmin2(oo, ro));
-    return de | (dd << 8);
-}
-
-template <int ND>
-__global__ __launch_bounds__(256) void ref_plane2_kernel(
-    const uint8_t* __restrict__ ref, const uint8_t* __restrict__ other, int W, int H, size_t pitch,
-    const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
-    const uint8_t* __restrict__ valid_in, int k, uint8_t* __restrict__ disp_u8,
-    uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out) {
-    __shared__ __attribute__((aligned(16))) uint8_t RT[64 * P2_RS];
-    __shared__ __attribute__((aligned(16))) uint8_t ADT[2][64 * P2_RS];
-    __shared__ unsigned bits[PT_MAXBITS / 32];
-    __shared__ __attribute__((aligned(16))) uint8_t OUT[P2_OU_BYTES];
-    __shared__ int box[4];                    // dx_lo, dx_hi, dy_lo, dy_hi
-    __shared__ unsigned short uniq[P2_ROWS * 64];   // pixels with a distinct relative line
-    __shared__ int nuniq;
-    const int t = threadIdx.x, lane = t & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int TW = PT_REG_W - 2 * k, w2 = 2 * k;
-    const int tx0 = k + blockIdx.x * TW, ty0 = k + blockIdx.y * P2_ROWS;
-    const int rx0 = tx0 - k, ry0 = ty0 - k;   // region origin (image coords)
-    const int RH = P2_ROWS + w2;
-#ifdef SVA_REF_PROF
-    long long tp[6];
-    int nplanes = 0;
-    tp[0] = clock64();
-#endif
-    if (t < 4) box[t] = (t & 1) ? -0x7fffffff : 0x7fffffff;
-    for (int i = t; i < RH * PT_REG_W; i += 256) {
-        const int v = i >> 6, u = i & 63;
-        const int gx = rx0 + u, gy = ry0 + v;
-        RT[u * P2_RS + v] = (gx < W && gy < H) ? ref[(size_t)gy * pitch + gx] : 0;
-    }
-    __syncthreads();
-    // this thread's pixels: column lane, rows 8 * wv + j.  All loads are
-    // issued first (clamped addresses), then used.
-    // Per-pixel membership terms (on_line restated per plane with 24-bit
-    // multiplies and no short-circuit): with ia = cx - x0, ib = cy - y0,
-    //   i = high ? ib : ia,  tt = step * (high ? ia : ib),  num = a*i + major - 1
-    //   on = i in [0, n) && (b == 0 ? tt == 0 : tt >= 0 && tt*b <= num < tt*b + b)
-    // n = 0 marks a pixel that is not evaluated.
-    int m_ox[8], m_oy[8], m_n[8], m_fl[8], m_a[8], m_b[8], m_mj[8];
-    bool ok[8];
-    int4 E[8];
-    unsigned long long best[8];
-    {
-        unsigned vin[8], mk[8];
-        const int xc = min(tx0 + lane, W - 1);
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const size_t p = (size_t)min(ty0 + 8 * wv + j, H - 1) * W + xc;
-            vin[j] = valid_in[p];
-            mk[j] = mask ? mask[p] : 1u;
-            E[j] = ends[p];
-        }
-        int bx0 = 0x7fffffff, bx1 = -0x7fffffff, by0 = 0x7fffffff, by1 = -0x7fffffff;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int x = tx0 + lane, y = ty0 + 8 * wv + j;
-            ok[j] = lane < TW && x < W - k && y < H - k && vin[j] != 0 && mk[j] != 0;
-            best[j] = ~0ull;
-            const Line L = make_line(E[j].x, E[j].y, E[j].z, E[j].w);
-            m_ox[j] = x - L.x0;
-            m_oy[j] = y - L.y0;
-            m_n[j] = ok[j] ? L.n : 0;
-            m_fl[j] = (L.high ? 1 : 0) | (L.step < 0 ? 2 : 0);
-            m_a[j] = L.a;
-            m_b[j] = L.b;
-            m_mj[j] = L.major - 1;
-            if (ok[j]) {
-                bx0 = min(bx0, min(E[j].x, E[j].z) - x);
-                bx1 = max(bx1, max(E[j].x, E[j].z) - x);
-                by0 = min(by0, min(E[j].y, E[j].w) - y);
-                by1 = max(by1, max(E[j].y, E[j].w) - y);
-            }
-        }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {   // wave min/max, then one atomic each
-            bx0 = min(bx0, __shfl_xor(bx0, off, 64));
-            bx1 = max(bx1, __shfl_xor(bx1, off, 64));
-            by0 = min(by0, __shfl_xor(by0, off, 64));
-            by1 = max(by1, __shfl_xor(by1, off, 64));
-        }
-        if (lane == 0) {
-            atomicMin(&box[0], bx0);
-            atomicMax(&box[1], bx1);
-            atomicMin(&box[2], by0);
-            atomicMax(&box[3], by1);
-        }
-    }
-    __syncthreads();
-    const int dxlo = box[0], dylo = box[2];
-    const int bw = box[1] - box[0] + 1, bh = box[3] - box[2] + 1;
-    if (box[1] < box[0]) return;             // no valid pixel in this tile
-    if ((long long)bw * bh > PT_MAXBITS) {
-        // offset box too large for the bitmap: per-pixel waves for this tile
-        for (int pi = wv; pi < TW * P2_ROWS; pi += 4) {
-            const int x = tx0 + pi % TW, y = ty0 + pi / TW;
-            if (x >= W - k || y >= H - k) continue;
-            const size_t p = (size_t)y * W + x;
-            if (!valid_in[p] || (mask && mask[p] == 0)) continue;
-            match_pixel_wave<ND>(ref, other, W, pitch, x, y, ends[p], k, disp_u8, disp_u16,
-                                 valid_out);
-        }
-        return;
-    }
-    const int nwords = (bw * bh + 31) >> 5;
-    for (int i = t; i < nwords; i += 256) bits[i] = 0;
-    if (t == 0) nuniq = 0;
-    __syncthreads();
-#ifdef SVA_REF_PROF
-    tp[1] = clock64();
-#endif
-    // Bresenham is translation-invariant: pixels whose endpoints, relative
-    // to themselves, match the left neighbour's or the previous row's have the
-    // same offset set.  Only the first of each such chain enters the list.
-    {
-        int4 prev = make_int4(0, 0, 0, 0);
-        bool prev_ok = false;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int x = tx0 + lane, y = ty0 + 8 * wv + j;
-            const int4 rel = make_int4(E[j].x - x, E[j].y - y, E[j].z - x, E[j].w - y);
-            const int lx = __shfl_up(rel.x, 1, 64), ly = __shfl_up(rel.y, 1, 64);
-            const int lz = __shfl_up(rel.z, 1, 64), lw = __shfl_up(rel.w, 1, 64);
-            const int lok = __shfl_up((int)ok[j], 1, 64);
-            const bool same_left = lane > 0 && lok && lx == rel.x && ly == rel.y && lz == rel.z &&
-                                   lw == rel.w;
-            const bool same_up = prev_ok && prev.x == rel.x && prev.y == rel.y &&
-                                 prev.z == rel.z && prev.w == rel.w;
-            if (ok[j] && !same_left && !same_up) uniq[atomicAdd(&nuniq, 1)] = (unsigned short)((8 * wv + j) * 64 + lane);
-            prev = rel;
-            prev_ok = ok[j];
-        }
-    }
-    __syncthreads();
-    // one thread per distinct line, walking it incrementally: the minor
-    // coordinate of point i is floor((a*i + major - 1) / b) with a <= b, so it
-    // advances by at most one per step (no division in the loop)
-    for (int q = t; q < nuniq; q += 256) {
-        const int pl = uniq[q], x = tx0 + (pl & 63), y = ty0 + (pl >> 6);
-        const int4 e = ends[(size_t)y * W + x];
-        const Line L = make_line(e.x, e.y, e.z, e.w);
-        int mnr = L.b > 0 ? (L.major - 1) / L.b : 0;
-        int rem = L.b > 0 ? (L.major - 1) - mnr * L.b : 0;
-        // bit of point i: (cy - y - dylo) * bw + (cx - x - dxlo)
-        const int bx0 = L.x0 - x - dxlo, by0 = L.y0 - y - dylo;
-        for (int i = 0; i < L.n; i++) {
-            const int off = L.step * mnr;
-            const int b = L.high ? (by0 + i) * bw + (bx0 + off) : (by0 + off) * bw + (bx0 + i);
-            atomicOr(&bits[b >> 5], 1u << (b & 31));
-            rem += L.a;
-            if (rem >= L.b) {
-                rem -= L.b;
-                mnr++;
-            }
-        }
-    }
-#ifdef SVA_REF_PROF
-    __syncthreads();
-    tp[2] = clock64();
-#endif
-    // O over the union of all planes, column-major: columns rx0 + dxlo +
-    // [0, 64 + bw - 1), rows ry0 + dylo + [0, RH + bh - 1), column stride os
-    // (odd dwords).  16 bytes of slack: bytes4() may touch one dword past a
-    // column, and the last rows of a 4-row group may run past RH.
-    const int ouw = PT_REG_W + bw - 1, ouh = RH + bh - 1 + 4;
-    const int os = ((((ouh + 3) >> 2) | 1) << 2);
-    const bool staged = ouw * os <= P2_OU_BYTES - 16;
-    if (staged) {
-        const int ox0 = rx0 + dxlo, oy0 = ry0 + dylo;
-        for (int i = t; i < ouw * ouh; i += 256) {
-            const int v = i / ouw, u = i - v * ouw;
-            const int gx = ox0 + u, gy = oy0 + v;
-            OUT[u * os + v] =
-                (gx >= 0 && gx < W && gy >= 0 && gy < H) ? other[(size_t)gy * pitch + gx] : 0;
-        }
-    }
-    const rsrc_t ro = make_rsrc(other, (unsigned)min((size_t)0xffffffffu, (size_t)H * pitch));
-    __syncthreads();
-#ifdef SVA_REF_PROF
-    tp[3] = clock64();
-#endif
-
-    // (a) AD plane of the region, column-major.  Thread (wave w, lane u)
-    // owns column u, row groups 4 * (w + 4q), q < 6 (RH <= 88 rows = 22
-    // groups); every read is issued unconditionally (addresses stay inside
-    // the LDS images), only the writes are guarded.
-    const int nv4 = (RH + 3) >> 2;
-    auto ad_plane = [&](int ddx, int ddy, uint8_t* adt) {
-        const int u = lane;
-        if (staged) {
-            const int ob = (u + ddx - dxlo) * os + (ddy - dylo);
-            unsigned o[6], r[6];
-#pragma unroll
-            for (int q = 0; q < 6; q++) {
-                const int v = 4 * min(wv + 4 * q, nv4 - 1);
-                o[q] = bytes4(OUT, ob + v);
-                r[q] = *reinterpret_cast<const unsigned*>(&RT[u * P2_RS + v]);
-            }
-#pragma unroll
-            for (int q = 0; q < 6; q++) {
-                const int v4 = wv + 4 * q;
-                if (v4 < nv4)
-                    *reinterpret_cast<unsigned*>(&adt[u * P2_RS + 4 * v4]) = absdiff4(o[q], r[q]);
-            }
-        } else {
-            const unsigned gx = (unsigned)(rx0 + u + ddx);
-            for (int v4 = wv; v4 < nv4; v4 += 4) {
-                const int v = 4 * v4;
-                const unsigned base = (unsigned)(ry0 + v + ddy) * (unsigned)pitch + gx;
-                unsigned o = 0;
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    o |= __builtin_amdgcn_raw_buffer_load_b8(ro, base + (unsigned)q * (unsigned)pitch,
-                                                             0, 0) << (8 * q);
-                const unsigned r = *reinterpret_cast<const unsigned*>(&RT[u * P2_RS + v]);
-                *reinterpret_cast<unsigned*>(&adt[u * P2_RS + v]) = absdiff4(o, r);
-            }
-        }
-    };
-    // (b) this wave's 8 output rows of one plane: column sums, SADs, keys
-    const int r0 = 8 * wv;
-    const int kh = w2 >> 2;                   // whole dwords in a 2k-row column sum
-    auto sad_rows = [&](int ddx, int ddy, const uint8_t* adt) {
-        const uint8_t* col = adt + lane * P2_RS;
-        const unsigned* cw = reinterpret_cast<const unsigned*>(col);
-        unsigned s = 0;
-        for (int q = 0; q < kh; q++) s = __builtin_amdgcn_sad_u8(cw[(r0 >> 2) + q], 0u, s);
-        if (w2 & 2) s = __builtin_amdgcn_sad_u8(cw[(r0 >> 2) + kh] & 0xffffu, 0u, s);
-        // rows leaving (r0 .. r0+6) and entering (r0+2k .. r0+2k+6)
-        const unsigned out0 = cw[r0 >> 2], out1 = cw[(r0 >> 2) + 1];
-        const unsigned in0 = bytes4(col, r0 + w2), in1 = bytes4(col, r0 + w2 + 4);
-        unsigned sj[8], sad[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            if (j > 0) {
-                const unsigned ow = j - 1 < 4 ? out0 : out1, iw = j - 1 < 4 ? in0 : in1;
-                const unsigned sh = 8u * (unsigned)((j - 1) & 3);
-                s = s + ((iw >> sh) & 0xffu) - ((ow >> sh) & 0xffu);
-            }
-            sj[j] = s;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) {        // 8 independent scans: interleaved
-            const unsigned P = scan64_dpp(sj[j]);
-            const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute((lane + w2 - 1) << 2, (int)P);
-            sad[j] = hi - P + sj[j];
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) {        // membership (on_line) + first-minimum key
-            const int ia = m_ox[j] + ddx, ib = m_oy[j] + ddy;
-            const int high = m_fl[j] & 1, neg = -((m_fl[j] >> 1) & 1);
-            const int i = high ? ib : ia;
-            const int u = high ? ia : ib;
-            const int tt = (u ^ neg) - neg;              // step * u, step = +-1
-            const int num = __mul24(m_a[j], i) + m_mj[j];
-            const int tb = __mul24(tt, m_b[j]);
-            const int in_range = (unsigned)i < (unsigned)m_n[j];
-            const int on_pt = (int)(tt == 0);
-            const int on_ln = (int)(tt >= 0) & (int)(tb <= num) & (int)(num < tb + m_b[j]);
-            const int on = in_range & (m_b[j] == 0 ? on_pt : on_ln);
-            const unsigned long long key = ((unsigned long long)sad[j] << 32) | (unsigned)i;
-            best[j] = (on & (int)(key < best[j])) ? key : best[j];
-        }
-    };
-    int wd = 0;
-    unsigned m = nwords > 0 ? bits[0] : 0u;  // uniform across the workgroup
-    auto next_plane = [&](int& ddx, int& ddy) -> bool {
-        while (m == 0) {
-            if (++wd >= nwords) return false;
-            m = bits[wd];
-        }
-        const int b = wd * 32 + __builtin_ctz(m);
-        m &= m - 1;
-        ddy = dylo + b / bw;
-        ddx = dxlo + b % bw;
-        return true;
-    };
-    for (;;) {
-        int ax, ay, bx, by;
-        const bool pa = next_plane(ax, ay);
-        if (!pa) break;
-        const bool pb = next_plane(bx, by);
-#ifdef SVA_REF_PROF
-        nplanes += 1 + (int)pb;
-#endif
-        ad_plane(ax, ay, ADT[0]);
-        if (pb) ad_plane(bx, by, ADT[1]);
-        __syncthreads();
-        sad_rows(ax, ay, ADT[0]);
-        if (pb) sad_rows(bx, by, ADT[1]);
-        __syncthreads();
-        if (!pb) break;
-    }
-#ifdef SVA_REF_PROF
-    tp[4] = clock64();
-#endif
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        if (!ok[j]) continue;
-        const int x = tx0 + lane, y = ty0 + r0 + j;
-        const size_t p = (size_t)y * W + x;
-        const int4 e = ends[p];
-        int cx, cy;
-        line_point(make_line(e.x, e.y, e.z, e.w), (int)(best[j] & 0xffffffffu), cx, cy);
-        const double dx = (double)(cx - x), dy = (double)(cy - y);
-        const int dn = (int)__builtin_sqrt(dx * dx + dy * dy);       // :89
-        disp_u8[p] = (uint8_t)dn;
-        if (disp_u16) disp_u16[p] = (uint16_t)dn;
-        if (valid_out) valid_out[p] = 1;
-    }
-#ifdef SVA_REF_PROF
-    tp[5] = clock64();
-    if (t == 0 && (blockIdx.x % 16) == 5 && (blockIdx.y % 8) == 3)
-        printf("REFPROF blk %d %d planes %d staged %d box %dx%d setup %lld bitmap %lld stage %lld planes %lld out %lld\n",
-               blockIdx.x, blockIdx.y, nplanes, (int)staged, bw, bh, tp[1] - tp[0], tp[2] - tp[1],
-               tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4]);
-#endif
-}
-
-// ---- offset-plane algorithm, v3 (the one launched) --------------------------
-// v2 spent most lanes on the window halo: a wave covered the 64 region
-// columns of a (64 - 2k)-pixel tile, so at k = 20 only 24 of 64 lanes owned
-// an output.  v3 gives every lane an output column:
+// ---- offset-plane algorithm (v3) ---------------------------------------------
+// The round-1 kernel (v2) spent most lanes on the window
+// halo: a wave covered the 64 region columns of a (64 - 2k)-pixel tile, so at
+// k = 20 only 24 of 64 lanes owned an output.  v3 gives every lane an output
+// column:
 //   * Tile = 64 output columns x 32 rows (wave w: rows 8w..8w+7); the region
 //     is 63 + 2k columns.  Lane u owns region columns u and u + 64 (the
 //     second is real for u < 2k - 1).  The 2k-column box sum reads the
@@ -595,8 +235,8 @@ __global__ __launch_bounds__(256) void ref_plane2_kernel(
 //   * No AD plane in LDS: the 2k-row column sums are v_sad_u8 of staged O
 //     dwords (column-major, 4 rows per dword, one wave-uniform v_alignbyte)
 //     against the lane's R dwords, which stay in registers for the whole
-//     tile; rows r0+1..r0+7 follow from masked v_sad_u8 of the leaving and
-//     entering rows.  Nothing is written to LDS per plane, so the four waves
+//     tile; rows r0+1..r0+7 follow from v_sad_u8 of the leaving and
+//     entering rows (partial dwords by byte select).  Nothing is written to LDS per plane, so the four waves
 //     run their plane loops with no barrier.
 //   * Membership is an interval test.  Planes are visited with the tile's
 //     dominant major axis innermost (row-major bitmap when most lines are
@@ -1080,31 +720,6 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
     const long long npx = (long long)(W - 2 * k) * (H - 2 * k);
     if (npx <= 0) return hipSuccess;
     if (k <= PT_MAXK) {   // offset-plane algorithm
-        // A/B switch for the previous plane kernel (tools/bench_refpath.py)
-        static const bool plane_v2 = [] {
-            const char* e = getenv("SVA_REF_PLANE");
-            return e && e[0] == '2';
-        }();
-        if (plane_v2) {
-            const int tw = PT_REG_W - 2 * k;
-            const dim3 pg2((unsigned)((W - 2 * k + tw - 1) / tw),
-                           (unsigned)((H - 2 * k + P2_ROWS - 1) / P2_ROWS));
-#define SVA_PLANE2_CASE(ND)                                                                    \
-    case ND:                                                                                   \
-        hipLaunchKernelGGL(ref_plane2_kernel<ND>, pg2, dim3(256), 0, c.stream, ref, other, W, H, \
-                           pitch, mask, (const int4*)ends, valid_in, k, disp_u8, disp_u16,      \
-                           valid_out);                                                         \
-        break;
-            switch ((k + 1) / 2) {
-                SVA_PLANE2_CASE(1) SVA_PLANE2_CASE(2) SVA_PLANE2_CASE(3) SVA_PLANE2_CASE(4)
-                SVA_PLANE2_CASE(5) SVA_PLANE2_CASE(6) SVA_PLANE2_CASE(7) SVA_PLANE2_CASE(8)
-                SVA_PLANE2_CASE(9) SVA_PLANE2_CASE(10) SVA_PLANE2_CASE(11) SVA_PLANE2_CASE(12)
-                SVA_PLANE2_CASE(13) SVA_PLANE2_CASE(14)
-                default: return hipErrorInvalidValue;
-            }
-#undef SVA_PLANE2_CASE
-            return hipGetLastError();
-        }
         const dim3 pg3((unsigned)((W - 2 * k + 63) / 64),
                        (unsigned)((H - 2 * k + P3_ROWS - 1) / P3_ROWS));
 #define SVA_PLANE3_CASE(K_)                                                                    \

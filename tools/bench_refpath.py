@@ -86,7 +86,7 @@ def main():
         cpu_rate = ncpu / cdt / 1e6
         del band
         digest = hashlib.sha1(d16.cpu().numpy().tobytes() + val.cpu().numpy().tobytes()).hexdigest()[:16]
-        out.append({"size": f"{W}x{H}", "pair": pair, "plane_kernel": os.environ.get("SVA_REF_PLANE", "3"),
+        out.append({"size": f"{W}x{H}", "pair": pair,
                     "out_sha1": digest, "candidates": int(n_cand), "gpu_ms": round(dt * 1e3, 3),
                     "ref_match_ms": round(ms_match / max(n, 1), 3),
                     "gpu_Mcand_per_s": round(gpu_rate, 1),
