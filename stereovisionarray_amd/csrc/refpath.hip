@@ -204,7 +204,9 @@ __global__ __launch_bounds__(256) void ref_match_kernel(
 //      whatever order the planes are visited in.
 // A tile whose offset geometry exceeds the kernel's buffers falls back to
 // match_pixel_wave.
-constexpr int PT_MAXK = 28;                  // largest k of the plane kernel
+// largest k of the plane kernel: the ABI maximum.  Region 63 + 2k <= 127
+// columns (two per lane) and SAD <= (2k)^2 * 255 < 2^20 for the u32 key.
+constexpr int PT_MAXK = 32;
 
 // Inclusive wave64 scan in 6 DPP adds (no LDS): Hillis-Steele within each
 // 16-lane row (row_shr 1, 2, 4, 8; lanes with no source read 0), then
@@ -244,7 +246,7 @@ __device__ __forceinline__ unsigned scan64_dpp(unsigned v) {
 //     on a pixel's line form one interval -- of length <= 1 when the pixel's
 //     own major axis is the outer one -- recomputed only when the outer
 //     offset changes.  Per plane the test is (d_in - lo) < len, and the
-//     first-minimum key is the u32 (SAD << 12 | i): SAD < 2^20 for k <= 28,
+//     first-minimum key is the u32 (SAD << 12 | i): SAD < 2^20 for k <= 32,
 //     i < 4096 (Mode R requires W, H < 4096).
 constexpr int P3_ROWS = 32;                          // 4 waves x 8 rows
 constexpr int P3_RW_MAX = 63 + 2 * PT_MAXK;          // region columns
@@ -321,6 +323,7 @@ __global__ __launch_bounds__(256, SVA_P3_MINB) void ref_plane3_kernel(
     constexpr int RS4 = P3_RS / 4;
     static_assert(24 + 4 * ND2 <= P3_RS, "R column stride too small");
     static_assert(ND2 >= ND + 2, "entering rows");
+    static_assert(4 * K * K * 255 < (1 << 20), "SAD must fit the 20-bit key field");
     __shared__ __attribute__((aligned(16))) uint8_t RT[P3_RW_MAX * P3_RS];
     __shared__ unsigned bits[P3_WORDS];
     __shared__ __attribute__((aligned(16))) uint8_t OUT[P3_OU_BYTES];
@@ -736,6 +739,7 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
             SVA_PLANE3_CASE(17) SVA_PLANE3_CASE(18) SVA_PLANE3_CASE(19) SVA_PLANE3_CASE(20)
             SVA_PLANE3_CASE(21) SVA_PLANE3_CASE(22) SVA_PLANE3_CASE(23) SVA_PLANE3_CASE(24)
             SVA_PLANE3_CASE(25) SVA_PLANE3_CASE(26) SVA_PLANE3_CASE(27) SVA_PLANE3_CASE(28)
+            SVA_PLANE3_CASE(29) SVA_PLANE3_CASE(30) SVA_PLANE3_CASE(31) SVA_PLANE3_CASE(32)
             default: return hipErrorInvalidValue;
         }
 #undef SVA_PLANE3_CASE

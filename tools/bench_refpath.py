@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu-rows", type=int, default=24, help="rows of the CPU sample")
     ap.add_argument("--pairs", default="12-11", help="reference-rig pairs, e.g. 12-11,12-7,12-6")
+    ap.add_argument("--k", type=int, default=20, help="kernelSize (2k x 2k windows)")
     a = ap.parse_args()
     import torch
     import stereovisionarray_amd as sva
@@ -41,7 +42,7 @@ def main():
     for spec, pair in [(s_, p_) for s_ in a.sizes.split(",") for p_ in a.pairs.split(",")]:
         W, H = map(int, spec.split("x"))
         i_ref, i_oth = map(int, pair.split("-"))
-        k = 20
+        k = a.k
         grid = synth.reference_array(0.036 / W)
         cr, co = sva.Camera.make(*grid[i_ref]), sva.Camera.make(*grid[i_oth])
         ocr, oco = pyoracle.OCamera.make(*grid[i_ref]), pyoracle.OCamera.make(*grid[i_oth])
@@ -86,7 +87,7 @@ def main():
         cpu_rate = ncpu / cdt / 1e6
         del band
         digest = hashlib.sha1(d16.cpu().numpy().tobytes() + val.cpu().numpy().tobytes()).hexdigest()[:16]
-        out.append({"size": f"{W}x{H}", "pair": pair,
+        out.append({"size": f"{W}x{H}", "pair": pair, "k": k,
                     "out_sha1": digest, "candidates": int(n_cand), "gpu_ms": round(dt * 1e3, 3),
                     "ref_match_ms": round(ms_match / max(n, 1), 3),
                     "gpu_Mcand_per_s": round(gpu_rate, 1),
