@@ -5,12 +5,11 @@
 //                         operand order (Camera.cpp:15-34,
 //                         CameraStereoVision.cpp:28,60-71).  FMA contraction
 //                         is off for this file so every rounding matches.
-//   ref_match_kernel      one wave per pixel, one lane per Bresenham
-//                         candidate (functions.cpp:253-321 in closed form),
-//                         2k x 2k SAD with v_sad_u8 (4 |a-b| per lane-op) on
-//                         dword-realigned rows (v_alignbyte), first-minimum
-//                         argmin as a wave-wide u64 min over (SAD << 32 | i),
-//                         then (uchar)(int)sqrt(dx^2 + dy^2)
+//   ref_plane3_kernel     the offset-plane algorithm (below) for every k the
+//                         ABI accepts (1..32), with a per-pixel fallback
+//                         (match_pixel_wave) for tiles whose offset geometry
+//                         exceeds its buffers; first-minimum argmin, then
+//                         (uchar)(int)sqrt(dx^2 + dy^2)
 //                         (CameraStereoVision.cpp:85-89).
 #pragma clang fp contract(off)
 
@@ -128,9 +127,11 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 
 // sad_row<ND>: sva_device.h
 
-// Per-pixel wave algorithm (one wave per reference pixel, one lane per
-// candidate, v_sad_u8 on v_alignbyte-realigned rows).  Used by
-// ref_match_kernel and as the per-tile fallback of ref_plane_kernel.
+// Per-pixel wave algorithm: one wave per reference pixel, one lane per
+// Bresenham candidate (functions.cpp:253-321 in closed form), the 2k x 2k SAD
+// with v_sad_u8 (4 |a-b| per lane-op) on v_alignbyte-realigned rows, and the
+// first minimum as a wave-wide u64 min over (SAD << 32 | i).  The per-tile
+// fallback of ref_plane3_kernel.
 template <int ND>
 __device__ __forceinline__ void match_pixel_wave(const uint8_t* __restrict__ ref,
                                                  const uint8_t* __restrict__ other, int W,
@@ -170,23 +171,6 @@ __device__ __forceinline__ void match_pixel_wave(const uint8_t* __restrict__ ref
         if (disp_u16) disp_u16[p] = (uint16_t)dn;
         if (valid_out) valid_out[p] = 1;
     }
-}
-
-template <int ND>
-__global__ __launch_bounds__(256) void ref_match_kernel(
-    const uint8_t* __restrict__ ref, const uint8_t* __restrict__ other, int W, int H, size_t pitch,
-    const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
-    const uint8_t* __restrict__ valid_in, int k, uint8_t* __restrict__ disp_u8,
-    uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out) {
-    // one wave per pixel of the loop region [k, W-k) x [k, H-k)
-    const int iw = W - 2 * k;
-    const long long q = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-    if (q >= (long long)iw * (H - 2 * k)) return;
-    const int y = k + (int)(q / iw), x = k + (int)(q % iw);
-    const size_t p = (size_t)y * W + x;
-    if (!valid_in[p]) return;
-    if (mask && mask[p] == 0) return;                                 // :53
-    match_pixel_wave<ND>(ref, other, W, pitch, x, y, ends[p], k, disp_u8, disp_u16, valid_out);
 }
 
 // ---- offset-plane algorithm (same results, far less work) -------------------
@@ -708,13 +692,6 @@ hipError_t launch_ref_endpoints(Ctx& c, int W, int H, const sva_camera& cref,
     return hipGetLastError();
 }
 
-#define SVA_REF_CASE(ND)                                                                       \
-    case ND:                                                                                   \
-        hipLaunchKernelGGL(ref_match_kernel<ND>, grid, dim3(256), 0, c.stream, ref, other, W, H, \
-                           pitch, mask, (const int4*)ends, valid_in, k, disp_u8, disp_u16,      \
-                           valid_out);                                                         \
-        break;
-
 hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, int W, int H,
                             size_t pitch, const uint8_t* mask, const int32_t* ends,
                             const uint8_t* valid_in, int k, uint8_t* disp_u8,
@@ -722,37 +699,27 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
     ScopedKernelTimer t(c, "ref_match");
     const long long npx = (long long)(W - 2 * k) * (H - 2 * k);
     if (npx <= 0) return hipSuccess;
-    if (k <= PT_MAXK) {   // offset-plane algorithm
-        const dim3 pg3((unsigned)((W - 2 * k + 63) / 64),
-                       (unsigned)((H - 2 * k + P3_ROWS - 1) / P3_ROWS));
+    // offset-plane algorithm for every k (sva_api checks 1 <= k <= 32)
+    const dim3 pg3((unsigned)((W - 2 * k + 63) / 64),
+                   (unsigned)((H - 2 * k + P3_ROWS - 1) / P3_ROWS));
 #define SVA_PLANE3_CASE(K_)                                                                    \
     case K_:                                                                                   \
         hipLaunchKernelGGL(ref_plane3_kernel<K_>, pg3, dim3(256), 0, c.stream, ref, other, W, H, \
                            pitch, mask, (const int4*)ends, valid_in, disp_u8, disp_u16,         \
                            valid_out);                                                         \
         break;
-        switch (k) {
-            SVA_PLANE3_CASE(1) SVA_PLANE3_CASE(2) SVA_PLANE3_CASE(3) SVA_PLANE3_CASE(4)
-            SVA_PLANE3_CASE(5) SVA_PLANE3_CASE(6) SVA_PLANE3_CASE(7) SVA_PLANE3_CASE(8)
-            SVA_PLANE3_CASE(9) SVA_PLANE3_CASE(10) SVA_PLANE3_CASE(11) SVA_PLANE3_CASE(12)
-            SVA_PLANE3_CASE(13) SVA_PLANE3_CASE(14) SVA_PLANE3_CASE(15) SVA_PLANE3_CASE(16)
-            SVA_PLANE3_CASE(17) SVA_PLANE3_CASE(18) SVA_PLANE3_CASE(19) SVA_PLANE3_CASE(20)
-            SVA_PLANE3_CASE(21) SVA_PLANE3_CASE(22) SVA_PLANE3_CASE(23) SVA_PLANE3_CASE(24)
-            SVA_PLANE3_CASE(25) SVA_PLANE3_CASE(26) SVA_PLANE3_CASE(27) SVA_PLANE3_CASE(28)
-            SVA_PLANE3_CASE(29) SVA_PLANE3_CASE(30) SVA_PLANE3_CASE(31) SVA_PLANE3_CASE(32)
-            default: return hipErrorInvalidValue;
-        }
-#undef SVA_PLANE3_CASE
-        return hipGetLastError();
-    }
-    dim3 grid((unsigned)((npx + 3) / 4));
-    switch ((k + 1) / 2) {  // ND = ceil(2k / 4)
-        SVA_REF_CASE(1) SVA_REF_CASE(2) SVA_REF_CASE(3) SVA_REF_CASE(4)
-        SVA_REF_CASE(5) SVA_REF_CASE(6) SVA_REF_CASE(7) SVA_REF_CASE(8)
-        SVA_REF_CASE(9) SVA_REF_CASE(10) SVA_REF_CASE(11) SVA_REF_CASE(12)
-        SVA_REF_CASE(13) SVA_REF_CASE(14) SVA_REF_CASE(15) SVA_REF_CASE(16)
+    switch (k) {
+        SVA_PLANE3_CASE(1) SVA_PLANE3_CASE(2) SVA_PLANE3_CASE(3) SVA_PLANE3_CASE(4)
+        SVA_PLANE3_CASE(5) SVA_PLANE3_CASE(6) SVA_PLANE3_CASE(7) SVA_PLANE3_CASE(8)
+        SVA_PLANE3_CASE(9) SVA_PLANE3_CASE(10) SVA_PLANE3_CASE(11) SVA_PLANE3_CASE(12)
+        SVA_PLANE3_CASE(13) SVA_PLANE3_CASE(14) SVA_PLANE3_CASE(15) SVA_PLANE3_CASE(16)
+        SVA_PLANE3_CASE(17) SVA_PLANE3_CASE(18) SVA_PLANE3_CASE(19) SVA_PLANE3_CASE(20)
+        SVA_PLANE3_CASE(21) SVA_PLANE3_CASE(22) SVA_PLANE3_CASE(23) SVA_PLANE3_CASE(24)
+        SVA_PLANE3_CASE(25) SVA_PLANE3_CASE(26) SVA_PLANE3_CASE(27) SVA_PLANE3_CASE(28)
+        SVA_PLANE3_CASE(29) SVA_PLANE3_CASE(30) SVA_PLANE3_CASE(31) SVA_PLANE3_CASE(32)
         default: return hipErrorInvalidValue;
     }
+#undef SVA_PLANE3_CASE
     return hipGetLastError();
 }
 
