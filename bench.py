@@ -67,7 +67,7 @@ def parse():
     ap.add_argument("--streams", type=int, default=0,
                     help="pairs of a step go round-robin to this many contexts, each with its "
                          "own HIP stream and workspaces, so pairs overlap (0 = auto: 2 when a "
-                         "rank has several pairs per step, else 1)")
+                         "rank has several pairs per step and D != 192, else 1)")
     ap.add_argument("--path-kernel", default="auto", choices=["auto", "cost_volume", "fused"],
                     help="sva_set_path_kernel (DESIGN.md §4.5); auto = the library's choice "
                          "(the cost-volume route)")
@@ -665,7 +665,10 @@ def main():
             raise SystemExit("total_pairs must divide evenly over the ranks")
         P = wl["total_pairs"] // world
     params = sva.default_params(D=D, dmin=0, dir=-1, subpixel=1)
-    n_streams = a.streams if a.streams > 0 else (2 if P > 1 else 1)
+    # Pairs overlap on 2 streams by default; at D=192 a second stream loses
+    # (1080p x 256 pairs: 1 stream 251.5K, 2 streams 244.1K Mdisp/s), at D=128
+    # and D=256 it gains 4 % / 2 % (profiles/r02_v9/streams_ab.txt).
+    n_streams = a.streams if a.streams > 0 else (1 if P == 1 or D == 192 else 2)
     path_kernel = a.path_kernel
     kern = {"auto": sva.SVA_PATH_KERNEL_AUTO, "cost_volume": sva.SVA_PATH_KERNEL_COST_VOLUME,
             "fused": sva.SVA_PATH_KERNEL_FUSED}[path_kernel]
