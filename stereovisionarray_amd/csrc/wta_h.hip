@@ -18,9 +18,9 @@
 // therefore S, d* and the sub-pixel value are bit-identical to the 8-volume
 // route (tests/test_wta_h_gpu.py).
 //
-// HBM bytes per disparity: 1 C read (the second pass re-reads the same
-// segment from L2) + 6 volume reads, against 8 volume reads for wta.hip --
-// and the path kernel writes 6 volumes instead of 8.
+// HBM bytes per disparity: 1 C read (the second pass takes the segment's cost
+// words from LDS) + 6 volume reads, against 8 volume reads for wta.hip -- and
+// the path kernel writes 6 volumes instead of 8.
 #include "sgm_common.h"
 #include "wta_common.h"
 
@@ -38,7 +38,7 @@ struct WtaHGeom {
     unsigned ckvol;   // bytes of one checkpoint plane [H][ns][D]
 };
 
-// Prefetch depth (steps) of the backward pass, which loads 7 u8 vectors per
+// Prefetch depth (steps) of the backward pass, which loads 6 u8 vectors per
 // step; the forward pass loads 1 and runs a deeper ring.
 #ifndef SVA_WTAH_PF1
 #define SVA_WTAH_PF1 8
@@ -46,11 +46,16 @@ struct WtaHGeom {
 #ifndef SVA_WTAH_PF2
 #define SVA_WTAH_PF2 4
 #endif
-template <int DPL> constexpr int pf_fwd() { return DPL <= 8 ? SVA_WTAH_PF1 : SVA_WTAH_PF1 / 2; }
-template <int DPL> constexpr int pf_bwd() { return DPL <= 8 ? SVA_WTAH_PF2 : SVA_WTAH_PF2 / 2; }
-// Cache policy of the six volume loads (their last use): nt keeps the stream
-// from evicting the segment's cost bytes, which the backward pass re-reads
-// from L2 (PMC: with default loads the kernel fetched C twice from HBM).
+#ifndef SVA_WTAH_PF1_WIDE
+#define SVA_WTAH_PF1_WIDE (SVA_WTAH_PF1 / 2)
+#endif
+#ifndef SVA_WTAH_PF2_WIDE   // D > 128: 4 beats 2 and 3 (1080p D=192 -2 %, 4K D=256 -2.4 %)
+#define SVA_WTAH_PF2_WIDE SVA_WTAH_PF2
+#endif
+template <int DPL> constexpr int pf_fwd() { return DPL <= 8 ? SVA_WTAH_PF1 : SVA_WTAH_PF1_WIDE; }
+template <int DPL> constexpr int pf_bwd() { return DPL <= 8 ? SVA_WTAH_PF2 : SVA_WTAH_PF2_WIDE; }
+// Cache policy of the six volume loads (their last use): nt, so the stream
+// does not evict the cost bytes other workgroups are still reading.
 #ifndef SVA_WTAH_VOL_AUX
 #define SVA_WTAH_VOL_AUX 2
 #endif
@@ -120,6 +125,11 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
         for (int j = 0; j < NP; j++) A[j] = 0u;   // L(q) = 0, m = 0  =>  L = C
         m = 0u;
     }
+    // The forward pass keeps the segment's cost words for the backward pass in
+    // LDS, lane-major per (pixel, word) so that accesses are conflict-free:
+    // re-reading C instead cost 2-5 % (it came from HBM a second time at D > 128).
+    __shared__ unsigned cseg[K * NW * HB];
+    const int tid = (int)threadIdx.x;
     unsigned LR[K][NW];
     Words<NW> r1[PF1];
 #pragma unroll
@@ -130,6 +140,8 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
         unsigned cw[NW];
 #pragma unroll
         for (int w = 0; w < NW; w++) cw[w] = r1[slot].w[w];
+#pragma unroll
+        for (int w = 0; w < NW; w++) cseg[(j * NW + w) * HB + tid] = cw[w];
         if (j < n) sgm_step<DPL>(cw, A, m, LR[j], P1, P2);
         if constexpr (j + PF1 < K) {
             __builtin_amdgcn_sched_barrier(0);
@@ -146,11 +158,9 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
         for (int j = 0; j < NP; j++) A[j] = 0u;
         m = 0u;
     }
-    Words<NW> rc[PF2];
     Words<NW> rv[PF2][6];
     auto issue = [&](int slot, int j) {
         const unsigned off = base + (unsigned)(x0 + j) * uD;
-        rc[slot] = bload<NW>(rC, off);
 #pragma unroll
         for (int r = 0; r < 6; r++) rv[slot][r] = bload<NW, SVA_WTAH_VOL_AUX>(rV[r], off);
     };
@@ -168,7 +178,7 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
         if (j < n) {
             unsigned cw[NW], ow[NW];
 #pragma unroll
-            for (int w = 0; w < NW; w++) cw[w] = rc[slot].w[w];
+            for (int w = 0; w < NW; w++) cw[w] = cseg[(j * NW + w) * HB + tid];
             sgm_step<DPL>(cw, A, m, ow, P1, P2);
             unsigned S[NP];
 #pragma unroll
