@@ -54,11 +54,11 @@ struct WtaHGeom {
 #endif
 template <int DPL> constexpr int pf_fwd() { return DPL <= 8 ? SVA_WTAH_PF1 : SVA_WTAH_PF1_WIDE; }
 template <int DPL> constexpr int pf_bwd() { return DPL <= 8 ? SVA_WTAH_PF2 : SVA_WTAH_PF2_WIDE; }
-// Cache policy of the six volume loads (their last use): nt, so the stream
-// does not evict the cost bytes other workgroups are still reading.
-#ifndef SVA_WTAH_VOL_AUX
-#define SVA_WTAH_VOL_AUX 2
-#endif
+// Cache policy of the six volume loads (their last use): nt above D = 64, so
+// the stream does not evict the cost bytes other workgroups are still reading
+// (default loads: +9 % at 1080p D=128, +12 % at 4K D=256); at D = 64 the
+// default policy is 9 % faster (profiles/r02_v9/ab_wtah_pf.log).
+template <int DPL> constexpr int vol_aux() { return DPL <= 4 ? 0 : 2; }
 
 template <int NW>
 __device__ __forceinline__ void unpack_add(const unsigned (&w)[NW], unsigned (&S)[2 * NW]) {
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
     auto issue = [&](int slot, int j) {
         const unsigned off = base + (unsigned)(x0 + j) * uD;
 #pragma unroll
-        for (int r = 0; r < 6; r++) rv[slot][r] = bload<NW, SVA_WTAH_VOL_AUX>(rV[r], off);
+        for (int r = 0; r < 6; r++) rv[slot][r] = bload<NW, vol_aux<DPL>()>(rV[r], off);
     };
 #pragma unroll
     for (int q = 0; q < PF2; q++) issue(q, K - 1 - q);
