@@ -1,0 +1,79 @@
+"""bench.py host logic that needs no GPU: where roofline.traffic comes from.
+
+The live source runs rocprofv3 PMC passes as child processes; it must not run
+at N > 1, inside a PMC child, or under a profiler, and a failed pass must
+leave the committed figure with the reason in traffic_source.
+"""
+import argparse
+import importlib.util
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def line(bench):
+    kernels = {"sgm_paths": {"avg_ms": 0.62}}
+    return {"roofline": bench.roofline_of(kernels, 1920, 1080, 128, "1080p_d128")}
+
+
+def args(pmc):
+    return argparse.Namespace(pmc=pmc, workload="1080p_d128", path_kernel="auto",
+                              pairs_per_rank=1)
+
+
+def test_committed_source(bench):
+    out = line(bench)
+    bench.attach_traffic(args("committed"), out, 1)
+    assert out["roofline"]["traffic_source"].startswith("committed")
+    assert out["roofline"]["traffic"] == bench.load_traffic("1080p_d128", "sgm_paths")
+
+
+def test_live_skipped_at_n_gt_1_and_under_profiler(bench, monkeypatch):
+    called = []
+    monkeypatch.setattr(bench, "live_traffic", lambda a: called.append(1) or {})
+    out = line(bench)
+    bench.attach_traffic(args("live"), out, 2)
+    monkeypatch.setenv("ROCPROF_KERNEL_TRACE", "1")
+    bench.attach_traffic(args("live"), out, 1)
+    monkeypatch.delenv("ROCPROF_KERNEL_TRACE")
+    monkeypatch.setenv("SVA_BENCH_PMC_CHILD", "1")
+    bench.attach_traffic(args("live"), out, 1)
+    assert not called
+    assert out["roofline"]["traffic_source"].startswith("committed")
+
+
+def test_live_failure_falls_back(bench, monkeypatch):
+    def boom(a):
+        raise RuntimeError("rocprofv3 --pmc FETCH_SIZE exited 137")
+    monkeypatch.delenv("SVA_BENCH_PMC_CHILD", raising=False)
+    for k in [k for k in os.environ if k.startswith("ROCPROF")]:
+        monkeypatch.delenv(k)
+    monkeypatch.setattr(bench, "live_traffic", boom)
+    out = line(bench)
+    bench.attach_traffic(args("live"), out, 1)
+    rf = out["roofline"]
+    assert "live PMC pass failed" in rf["traffic_source"] and "137" in rf["traffic_source"]
+    assert rf["traffic"] == bench.load_traffic("1080p_d128", "sgm_paths")
+
+
+def test_live_success_uses_kernel_bytes(bench, monkeypatch):
+    monkeypatch.delenv("SVA_BENCH_PMC_CHILD", raising=False)
+    for k in [k for k in os.environ if k.startswith("ROCPROF")]:
+        monkeypatch.delenv(k)
+    kern = {"sgm_paths": {"hbm_read_bytes": 2, "hbm_write_bytes": 1, "hbm_bytes_per_launch": 3}}
+    monkeypatch.setattr(bench, "live_traffic", lambda a: kern)
+    out = line(bench)
+    bench.attach_traffic(args("live"), out, 1)
+    rf = out["roofline"]
+    assert rf["traffic"] == 3 and rf["traffic_source"].startswith("live")
+    assert rf["traffic_per_kernel"] == kern

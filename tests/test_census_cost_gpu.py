@@ -93,12 +93,15 @@ def test_census_cost_pitched(ctx, sva, oracle, torch_dev):
     assert np.array_equal(got, want)
 
 
-def test_census_cost_matches_split_kernels(ctx, sva, torch_dev):
-    # the same bytes as the two-kernel route (census x2 -> cost), 1080p D=128
-    W, H, D = 1920, 1080, 128
-    L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=1)
+@pytest.mark.parametrize("D,dir,dmin", [(128, -1, 0), (128, 1, 0), (64, -1, 5), (192, 1, 3),
+                                        (256, -1, 0)])
+def test_census_cost_matches_split_kernels(ctx, sva, torch_dev, D, dir, dmin):
+    # the same bytes as the two-kernel route (census x2 -> cost) at 1080p: the
+    # row sweep's 15 chunks per row, ring wrap-around and both border chunks
+    W, H = 1920, 1080
+    L, R, _ = synth.stereo_pair(H, W, D, dmin, dir, seed=1)
     dL, dR = dev(L, torch_dev), dev(R, torch_dev)
-    p = sva.default_params(D=D)
+    p = sva.default_params(D=D, dmin=dmin, dir=dir)
     cl = torch.zeros((H, W), dtype=torch.int64, device=torch_dev)
     cr = torch.zeros((H, W), dtype=torch.int64, device=torch_dev)
     C1 = torch.zeros((H, W, D), dtype=torch.uint8, device=torch_dev)

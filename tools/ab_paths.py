@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--H", type=int, default=1080)
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--dir", type=int, default=-1)
+    ap.add_argument("--dmin", type=int, default=0)
     ap.add_argument("--entry", default="paths",
                     choices=["paths", "sgm", "cost", "fused", "census", "census_cost", "ckpt",
                              "wta_h"])
@@ -46,7 +48,7 @@ def main():
     L8 = torch.zeros((8, H, W, D), dtype=torch.uint8, device=dev)
     ns, _ = sva.ckpt_segments(W, D)
     CK = torch.zeros((2, H, ns, D), dtype=torch.uint8, device=dev)
-    p = sva.default_params(D=D)
+    p = sva.default_params(D=D, dmin=a.dmin, dir=a.dir)
     handles = []
     for path in a.libs:
         lib = ct.CDLL(os.path.abspath(path))
@@ -67,6 +69,8 @@ def main():
     lib0.sva_census_d(h0, ct.c_void_p(dR.data_ptr()), W, H, ct.c_size_t(W), ct.c_void_p(cr.data_ptr()))
     lib0.sva_cost_d(h0, ct.c_void_p(cl.data_ptr()), ct.c_void_p(cr.data_ptr()), W, H, ct.byref(p),
                     ct.c_void_p(C_src.data_ptr()))
+    torch.cuda.synchronize()
+    C_ref = C_src.clone()          # census -> cost bytes, checked against every census_cost variant
     # checkpoint-mode volumes for the wta_h entry (first library)
     lib0.sva_paths_ckpt_d(h0, ct.c_void_p(C_src.data_ptr()), W, H, ct.byref(p),
                           ct.c_void_p(L8.data_ptr()), ct.c_void_p(CK.data_ptr()))
@@ -108,11 +112,10 @@ def main():
             e1.record(s)
             assert st == 0, (n, st)
             e1.synchronize()
+            if a.entry == "census_cost" and it == 0:
+                assert torch.equal(C, C_ref), f"{n}: census_cost differs from census -> cost"
             if it >= 2:
                 times[n].append(e0.elapsed_time(e1))
-        if a.entry == "census_cost" and it == 0:   # same bytes as census x2 -> cost
-            torch.cuda.synchronize()
-            assert torch.equal(C, C_src), "census_cost differs from census -> cost"
         if a.entry == "cost" and it == 0:
             outs = []
             for n, lib, h in handles:
