@@ -48,6 +48,7 @@ inline int seg_log2_of(int D) { return D <= 128 ? 5 : 4; }
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
+
 // Path volumes are written non-temporally (buffer aux bit nt = 2).  Measured
 // A/B (1080p D=128, interleaved runs, ablation variants 0/13): sgm_paths
 // 0.826-0.829 -> 0.747-0.774 ms, and the following wta 0.38 -> 0.35 ms.  With
@@ -157,22 +158,35 @@ __device__ __forceinline__ unsigned min3_u16x2(unsigned a, unsigned b, unsigned 
 //   L(p,d) = u + C(p,d) - m  = v_add3_u32(u, c, -(m * 0x10001))
 // The add3 is exact per 16-bit half: u_lo >= m makes the low half carry
 // exactly once, which the high half's (0xffff - m) absorbs.
+// Row-edge registers of the d-1 / d+1 neighbour shifts.  A DPP row shift
+// leaves the lane without a source (lane 0 for row_shr, 15 for row_shl) at
+// its old value, so registers that start as INF keep INF there for the whole
+// line when each step's shift takes the previous step's register as its old
+// value: no INF re-materialisation per step.
+struct Edges {
+    unsigned X = INF2, Y = INF2;
+};
+
 template <int DPL>
 __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigned (&A)[DPL / 2],
                                            unsigned& m, unsigned (&ow)[DPL / 4], unsigned P1,
-                                           unsigned P2) {
+                                           unsigned P2, Edges& e) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
     // neighbours: X = lane k-1's last pair, Y = lane k+1's first pair
-    const unsigned X = row_shr1(A[NP - 1], INF2);
-    const unsigned Y = row_shl1(A[0], INF2);
+    e.X = row_shr1(A[NP - 1], e.X);
+    e.Y = row_shl1(A[0], e.Y);
+    const unsigned X = e.X, Y = e.Y;
     unsigned M[NP];
     M[0] = __builtin_amdgcn_alignbit(A[0], X, 16);
 #pragma unroll
     for (int j = 1; j < NP; j++) M[j] = __builtin_amdgcn_alignbit(A[j], A[j - 1], 16);
     const unsigned Qlast = __builtin_amdgcn_alignbit(Y, A[NP - 1], 16);
-    const unsigned m2 = m | (m << 16);
-    const unsigned mP2 = m2 + P2 * 0x10001u;
-    const unsigned K = 0u - m2;
+    // K = -(m * 0x10001) in one v_mul_i32_i24 (m < 2^10; the literal's low 24
+    // bits are -65537), and m + P2 in both halves = P2 * 0x10001 - K: two VALU
+    // where m | m << 16, its negation and the sum took three plus a copy of P2
+    unsigned K;
+    asm("v_mul_i32_i24_e32 %0, 0xfffeffff, %1" : "=v"(K) : "v"(m));
+    const unsigned mP2 = P2 * 0x10001u - K;
     // Stage-major over the NP independent pairs, and a min TREE below: each
     // packed op's result is consumed one pair later, not by the next
     // instruction (gfx950 puts an s_nop between dependent VOP3P ops).
@@ -207,15 +221,23 @@ __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigne
     m = row_min_u32(mf.x < mf.y ? mf.x : mf.y);
 }
 
+template <int DPL>
+__device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigned (&A)[DPL / 2],
+                                           unsigned& m, unsigned (&ow)[DPL / 4], unsigned P1,
+                                           unsigned P2) {
+    Edges e;
+    sgm_step_c<DPL>(c, A, m, ow, P1, P2, e);
+}
+
 // The same step on u8-packed cost words (DPL/4 dwords of 4 disparities).
 template <int DPL>
 __device__ __forceinline__ void sgm_step(const unsigned (&cw)[DPL / 4], unsigned (&A)[DPL / 2],
                                          unsigned& m, unsigned (&ow)[DPL / 4], unsigned P1,
-                                         unsigned P2) {
+                                         unsigned P2, Edges& e) {
     unsigned c[DPL / 2];
 #pragma unroll
     for (int w = 0; w < DPL / 4; w++) unpack4(cw[w], c[2 * w], c[2 * w + 1]);
-    sgm_step_c<DPL>(c, A, m, ow, P1, P2);
+    sgm_step_c<DPL>(c, A, m, ow, P1, P2, e);
 }
 
 // Direction table, identical to oracle svo_direction().
@@ -316,6 +338,7 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
 #pragma unroll
     for (int j = 0; j < NP; j++) A[j] = 0u;   // L(q) = 0, m = 0  =>  L = C
     unsigned m = 0u;
+    Edges edges;
 
     Words<NW> ring[PF];
 #pragma unroll
@@ -350,7 +373,7 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
 #pragma unroll
         for (int w = 0; w < NW; w++) cw[w] = ring[p].w[w];
         unsigned ow[NW];
-        sgm_step<DPL>(cw, A, m, ow, P1, P2);
+        sgm_step<DPL>(cw, A, m, ow, P1, P2, edges);
         if constexpr (CKPT) {
             // ts is the (wave-uniform) step index; x the pixel just computed
             const int x = rx > 0 ? ts : W - 1 - ts;

@@ -117,6 +117,7 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
     const unsigned ckrow = (unsigned)y * (unsigned)g.ns;
 
     unsigned A[NP], m;
+    Edges edges;
     // ---- pass 1: left-to-right (direction 0) over the segment ------------
     if (s > 0) {
         load_state<DPL>(rCK0, (ckrow + (unsigned)(s - 1)) * uD + (unsigned)(k * DPL), A, m);
@@ -142,7 +143,7 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
         for (int w = 0; w < NW; w++) cw[w] = r1[slot].w[w];
 #pragma unroll
         for (int w = 0; w < NW; w++) cseg[(j * NW + w) * HB + tid] = cw[w];
-        if (j < n) sgm_step<DPL>(cw, A, m, LR[j], P1, P2);
+        if (j < n) sgm_step<DPL>(cw, A, m, LR[j], P1, P2, edges);
         if constexpr (j + PF1 < K) {
             __builtin_amdgcn_sched_barrier(0);
             r1[slot] = bload<NW>(rC, base + (unsigned)(x0 + j + PF1) * uD);
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
             unsigned cw[NW], ow[NW];
 #pragma unroll
             for (int w = 0; w < NW; w++) cw[w] = cseg[(j * NW + w) * HB + tid];
-            sgm_step<DPL>(cw, A, m, ow, P1, P2);
+            sgm_step<DPL>(cw, A, m, ow, P1, P2, edges);
             unsigned S[NP];
 #pragma unroll
             for (int p = 0; p < NP; p++) S[p] = A[p];      // L_1 (u16 pairs, < 256)
