@@ -19,11 +19,25 @@ __device__ __forceinline__ unsigned row_or_u32(unsigned v) {
     return v;
 }
 
-// Returns d* (0-based, the same in all 16 lanes of the row) and, when
-// want_sub, the f32 sub-pixel disparity dmin + d* (+ parabola offset) in *v.
+// The parabola through S(d*-1), S(d*), S(d*+1), in f32:
+// dmin + d* (+ (a - c) / (2 (a - 2b + c)) when 0 < d* < D-1 and the
+// denominator is positive).
+__device__ __forceinline__ float subpixel(int dmin, int ds, int D, unsigned a, unsigned b,
+                                          unsigned c) {
+    float r = (float)(dmin + ds);
+    if (ds > 0 && ds < D - 1) {
+        const int den = (int)a - 2 * (int)b + (int)c;
+        if (den > 0) r = r + (float)((int)a - (int)c) / (float)(2 * den);
+    }
+    return r;
+}
+
+// First-minimum WTA on the row: returns d* (0-based, the same in all 16
+// lanes) and, when want_sub, S(d*-1), S(d*), S(d*+1) in *sm, *s0, *sp (all
+// lanes; S outside [0, D) reads 0, unused by subpixel()).
 template <int DPL>
-__device__ __forceinline__ int wta_pick(const unsigned (&S)[DPL / 2], int k, int D, int dmin,
-                                        bool want_sub, float* v) {
+__device__ __forceinline__ int wta_pick_raw(const unsigned (&S)[DPL / 2], int k, bool want_sub,
+                                            unsigned* sm, unsigned* s0, unsigned* sp) {
     constexpr int NP = DPL / 2;
     const int d0 = k * DPL;
     unsigned best = 0xffffffffu;
@@ -36,7 +50,6 @@ __device__ __forceinline__ int wta_pick(const unsigned (&S)[DPL / 2], int k, int
     }
     best = row_min_u32(best);
     const int ds = (int)(best & 0xffffu);
-    float r = (float)(dmin + ds);
     if (want_sub) {
         unsigned vm = 0, vp = 0;
 #pragma unroll
@@ -48,15 +61,21 @@ __device__ __forceinline__ int wta_pick(const unsigned (&S)[DPL / 2], int k, int
             vp = (da == ds + 1) ? lo : vp;
             vp = (da + 1 == ds + 1) ? hi : vp;
         }
-        vm = row_or_u32(vm);
-        vp = row_or_u32(vp);
-        if (ds > 0 && ds < D - 1) {
-            const int a = (int)vm, b = (int)(best >> 16), c = (int)vp;
-            const int den = a - 2 * b + c;
-            if (den > 0) r = r + (float)(a - c) / (float)(2 * den);
-        }
+        *sm = row_or_u32(vm);
+        *sp = row_or_u32(vp);
+        *s0 = best >> 16;
     }
-    *v = r;
+    return ds;
+}
+
+// Returns d* (0-based, the same in all 16 lanes of the row) and, when
+// want_sub, the f32 sub-pixel disparity dmin + d* (+ parabola offset) in *v.
+template <int DPL>
+__device__ __forceinline__ int wta_pick(const unsigned (&S)[DPL / 2], int k, int D, int dmin,
+                                        bool want_sub, float* v) {
+    unsigned a = 0, b = 0, c = 0;
+    const int ds = wta_pick_raw<DPL>(S, k, want_sub, &a, &b, &c);
+    *v = want_sub ? subpixel(dmin, ds, D, a, b, c) : (float)(dmin + ds);
     return ds;
 }
 

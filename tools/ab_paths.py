@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--dir", type=int, default=-1)
+    ap.add_argument("--sub", action="store_true", help="wta_h / sgm entries: also write the f32 sub-pixel map")
     ap.add_argument("--dmin", type=int, default=0)
     ap.add_argument("--entry", default="paths",
                     choices=["paths", "sgm", "cost", "fused", "census", "census_cost", "ckpt",
@@ -44,11 +45,12 @@ def main():
     L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=1)
     dL, dR = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
     disp = torch.zeros((H, W), dtype=torch.int16, device=dev)
+    subm = torch.zeros((H, W), dtype=torch.float32, device=dev)
     C = torch.zeros((H, W, D), dtype=torch.uint8, device=dev)
     L8 = torch.zeros((8, H, W, D), dtype=torch.uint8, device=dev)
     ns, _ = sva.ckpt_segments(W, D)
     CK = torch.zeros((2, H, ns, D), dtype=torch.uint8, device=dev)
-    p = sva.default_params(D=D, dmin=a.dmin, dir=a.dir)
+    p = sva.default_params(D=D, dmin=a.dmin, dir=a.dir, subpixel=1 if a.sub else 0)
     handles = []
     for path in a.libs:
         lib = ct.CDLL(os.path.abspath(path))
@@ -90,7 +92,8 @@ def main():
             elif a.entry == "wta_h":
                 st = lib.sva_wta_h_d(h, ct.c_void_p(C.data_ptr()), ct.c_void_p(L8.data_ptr()),
                                      ct.c_void_p(CK.data_ptr()), W, H, ct.byref(p),
-                                     ct.c_void_p(disp.data_ptr()), None)
+                                     ct.c_void_p(disp.data_ptr()),
+                                     ct.c_void_p(subm.data_ptr()) if a.sub else None)
             elif a.entry == "census":
                 st = lib.sva_census_d(h, ct.c_void_p(dL.data_ptr()), W, H, ct.c_size_t(W),
                                       ct.c_void_p(cl.data_ptr()))
@@ -108,7 +111,8 @@ def main():
             else:
                 st = lib.sva_disparity_sgm_d(h, ct.c_void_p(dL.data_ptr()), ct.c_void_p(dR.data_ptr()),
                                              W, H, ct.c_size_t(W), ct.byref(p),
-                                             ct.c_void_p(disp.data_ptr()), None)
+                                             ct.c_void_p(disp.data_ptr()),
+                                             ct.c_void_p(subm.data_ptr()) if a.sub else None)
             e1.record(s)
             assert st == 0, (n, st)
             e1.synchronize()
@@ -142,11 +146,14 @@ def main():
                 else:
                     lib.sva_wta_h_d(h, ct.c_void_p(C.data_ptr()), ct.c_void_p(L8.data_ptr()),
                                     ct.c_void_p(CK.data_ptr()), W, H, ct.byref(p),
-                                    ct.c_void_p(disp.data_ptr()), None)
+                                    ct.c_void_p(disp.data_ptr()),
+                                    ct.c_void_p(subm.data_ptr()) if a.sub else None)
                 torch.cuda.synchronize()
                 t = L8 if a.entry == "ckpt" else disp
                 outs.append(torch.sum(t.view(torch.int64) if t.dtype == torch.uint8 else
                                       t.to(torch.int64)).item())
+                if a.entry == "wta_h" and a.sub:      # sub-pixel maps bit-identical
+                    outs[-1] = (outs[-1], torch.sum(subm.view(torch.int32).to(torch.int64)).item())
             if not os.environ.get("AB_NOCHECK"):     # ablation builds compute other values
                 assert len(set(outs)) == 1, outs
         if a.entry == "paths" and it == 0:
