@@ -33,11 +33,15 @@ __device__ __forceinline__ float subpixel(int dmin, int ds, int D, unsigned a, u
 }
 
 // First-minimum WTA on the row: returns d* (0-based, the same in all 16
-// lanes) and, when want_sub, S(d*-1), S(d*), S(d*+1) in *sm, *s0, *sp (all
-// lanes; S outside [0, D) reads 0, unused by subpixel()).
+// lanes) and, when want_sub, S(d*-1) | S(d*+1) << 16 in *spm and S(d*) in
+// *s0 (all lanes; a neighbour outside [0, D) reads 0, unused by subpixel()).
+// d*-1 and d*+1 have the same parity, so they sit in the same half of two
+// adjacent pairs: each lane selects pair q = (d*-1-d0) >> 1 and q + 1 of
+// its own (zero outside the lane) and one v_perm packs the two halves; a
+// single DPP OR-reduction then gathers both values.
 template <int DPL>
 __device__ __forceinline__ int wta_pick_raw(const unsigned (&S)[DPL / 2], int k, bool want_sub,
-                                            unsigned* sm, unsigned* s0, unsigned* sp) {
+                                            unsigned* spm, unsigned* s0) {
     constexpr int NP = DPL / 2;
     const int d0 = k * DPL;
     unsigned best = 0xffffffffu;
@@ -51,18 +55,16 @@ __device__ __forceinline__ int wta_pick_raw(const unsigned (&S)[DPL / 2], int k,
     best = row_min_u32(best);
     const int ds = (int)(best & 0xffffu);
     if (want_sub) {
-        unsigned vm = 0, vp = 0;
+        const int im = ds - 1 - d0;             // local index of d*-1 (may leave the lane)
+        const int q = im >> 1;                  // arithmetic shift: -1 for im in {-2, -1}
+        unsigned pm = 0, pp = 0;
 #pragma unroll
         for (int j = 0; j < NP; j++) {
-            const int da = d0 + 2 * j;
-            const unsigned lo = S[j] & 0xffffu, hi = S[j] >> 16;
-            vm = (da == ds - 1) ? lo : vm;
-            vm = (da + 1 == ds - 1) ? hi : vm;
-            vp = (da == ds + 1) ? lo : vp;
-            vp = (da + 1 == ds + 1) ? hi : vp;
+            pm = (q == j) ? S[j] : pm;
+            pp = (q == j - 1) ? S[j] : pp;
         }
-        *sm = row_or_u32(vm);
-        *sp = row_or_u32(vp);
+        const unsigned sel = (im & 1) ? 0x07060302u : 0x05040100u;
+        *spm = row_or_u32(__builtin_amdgcn_perm(pp, pm, sel));
         *s0 = best >> 16;
     }
     return ds;
@@ -73,9 +75,9 @@ __device__ __forceinline__ int wta_pick_raw(const unsigned (&S)[DPL / 2], int k,
 template <int DPL>
 __device__ __forceinline__ int wta_pick(const unsigned (&S)[DPL / 2], int k, int D, int dmin,
                                         bool want_sub, float* v) {
-    unsigned a = 0, b = 0, c = 0;
-    const int ds = wta_pick_raw<DPL>(S, k, want_sub, &a, &b, &c);
-    *v = want_sub ? subpixel(dmin, ds, D, a, b, c) : (float)(dmin + ds);
+    unsigned spm = 0, b = 0;
+    const int ds = wta_pick_raw<DPL>(S, k, want_sub, &spm, &b);
+    *v = want_sub ? subpixel(dmin, ds, D, spm & 0xffffu, b, spm >> 16) : (float)(dmin + ds);
     return ds;
 }
 

@@ -169,9 +169,9 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
     for (int q = 0; q < PF2; q++) issue(q, K - 1 - q);
     // per owned pixel: d* and S(d*-1), S(d*), S(d*+1); the owning lane forms
     // the sub-pixel value after the loop (one division per pixel, not 16)
-    unsigned dres[R], sres[R][3];
+    unsigned dres[R], sres[R][2];
 #pragma unroll
-    for (int e = 0; e < R; e++) dres[e] = sres[e][0] = sres[e][1] = sres[e][2] = 0u;
+    for (int e = 0; e < R; e++) dres[e] = sres[e][0] = sres[e][1] = 0u;
     const bool want_sub = sub != nullptr;
     for_seq<K>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
@@ -188,13 +188,12 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
             unpack_add<NW>(LR[j], S);                        // L_0
 #pragma unroll
             for (int r = 0; r < 6; r++) unpack_add<NW>(rv[slot][r].w, S);
-            unsigned sm, s0, sp;
-            const int ds = wta_pick_raw<DPL>(S, k, want_sub, &sm, &s0, &sp);
+            unsigned spm, s0;
+            const int ds = wta_pick_raw<DPL>(S, k, want_sub, &spm, &s0);
             if (k == j / R) {
                 dres[j % R] = (unsigned)ds;
-                sres[j % R][0] = sm;
+                sres[j % R][0] = spm;
                 sres[j % R][1] = s0;
-                sres[j % R][2] = sp;
             }
         }
         if constexpr (j - PF2 >= 0) {
@@ -210,7 +209,8 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
         if (x < W) {
             disp[row + x] = (uint16_t)(g.dmin + (int)dres[e]);
             if (want_sub)
-                sub[row + x] = subpixel(g.dmin, (int)dres[e], D, sres[e][0], sres[e][1], sres[e][2]);
+                sub[row + x] = subpixel(g.dmin, (int)dres[e], D, sres[e][0] & 0xffffu, sres[e][1],
+                                        sres[e][0] >> 16);
         }
     }
 }
