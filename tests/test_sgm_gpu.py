@@ -226,6 +226,20 @@ def test_full_size_1080p_d128(ctx, sva, oracle):
 
 
 @pytest.mark.slow
+def test_full_size_4k_d256(ctx, sva, oracle):
+    """BASELINE config 3 at full size (3840x2160, D=256, seed 2):
+    bit-exact vs the threaded oracle on the default route, which is the route
+    bench.py times for this workload (~9 GB of oracle buffers, ~15 s)."""
+    W, H, D = 3840, 2160, 256
+    L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=2)
+    p = sva.default_params(D=D, subpixel=1)
+    disp, sub = ctx.disparity_sgm(L, R, p)
+    od, osub = oracle.sgm(L, R, D, 0, -1, subpixel=True, threads=16)
+    assert np.array_equal(disp, od)
+    assert np.max(np.abs(sub - osub)) <= SUB_TOL
+
+
+@pytest.mark.slow
 def test_full_size_4k_d256_properties(ctx, sva):
     """BASELINE config 3 (3840x2160, D=256): size-independent properties --
     deterministic across runs, and exact d0 on a constant-shift texture."""
