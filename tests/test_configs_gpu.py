@@ -1,11 +1,12 @@
-"""BASELINE.json configs 4 and 5 at full size (VERDICT r01 "next" #1).
+"""BASELINE.json configs 4 and 5 at full size (VERDICT r01 "next" #1, r02 #1).
 
-Config 4 -- 8-camera array at 1080p D=128, gather + fuse.  SURVEY.md §8d
-spells it as getCameraPairs(TO_CENTER_SMALL) = 12 <-> {6,7,8,11,13,16,17,18}
-(/root/reference/src/functions.cpp:156-165), each pair matched along its own
-baseline step, then the 8-map median depth (§2.6).  Every
-map is bit-exact vs the threaded oracle (oracle.sgm2), and the fused depth is
-bit-exact in f64 vs oracle.fuse_depth.
+Config 4 -- 8-camera array at 1080p D=128, gather + fuse, in both spellings:
+SURVEY.md §8d's getCameraPairs(TO_CENTER_SMALL) = 12 <-> {6,7,8,11,13,16,17,18}
+(/root/reference/src/functions.cpp:156-165), and BASELINE's own wording, a
+2 x 4 grid with all 28 pairwise baselines (bench.py's grid8_all).  Each pair
+is matched along its own baseline step, then the per-camera
+median depth (§2.6).  Every map is bit-exact vs the threaded oracle
+(oracle.sgm2), and every fused depth is bit-exact in f64 vs oracle.fuse_depth.
 
 Config 5 -- 256 x 1080p D=192 pairs.  One pair bit-exact vs oracle.sgm through
 BOTH path kernels (cost volume and census-fused), and bench.py's batch route
@@ -82,6 +83,75 @@ def test_config4_center8_fusion(ctx, sva, oracle, center8_views):
     assert np.array_equal(nv, en)
     assert np.array_equal(depth.view(np.uint64), exp.view(np.uint64))
     assert (nv == 8).mean() > 0.5
+
+
+# Config 4 in BASELINE's own wording (bench.py --workload grid8_all): an
+# 8-camera array (2 x 4 grid), all 28 pairwise baselines at 1080p D=128, each
+# matched along its reduced grid step.  The distinct steps are (-3,-1),
+# (-2,-1), (-1,-1), (-1,0) at k = 1, 2, 3, (0,-1), (1,-1), (2,-1), (3,-1); every
+# pair is compared with the threaded oracle, then the 7 per-camera median
+# fusions (camera i fuses its pairs (i, j > i)) bit-exact in f64.
+GRID8_PAIRS = synth.array_pairs(8)
+
+
+@pytest.fixture(scope="module")
+def grid8_views():
+    D = 128
+    g = synth.array_grid(2, 4)
+    kmax = max(synth.pair_step(g[i], g[j])[2] for i, j in GRID8_PAIRS)
+    dmax = min((D - 1) // kmax, 100)
+    delta = synth.array_delta(H, W, dmax)
+    views = synth.array_views(H, W, g, delta, seed=7)     # bench.py's grid8_all scene
+    return g, views, {}
+
+
+def test_grid8_all_steps_cover_the_verdict_list():
+    g = synth.array_grid(2, 4)
+    steps = {synth.pair_step(g[i], g[j]) for i, j in GRID8_PAIRS}
+    assert {(sx, sy) for sx, sy, _ in steps} == {(-3, -1), (-2, -1), (-1, -1), (-1, 0), (0, -1),
+                                                 (1, -1), (2, -1), (3, -1)}
+    assert {k for sx, sy, k in steps if (sx, sy) == (-1, 0)} == {1, 2, 3}
+
+
+@pytest.mark.parametrize("u", range(len(GRID8_PAIRS)))
+def test_config4_grid8_all_pair(ctx, sva, oracle, grid8_views, u):
+    g, views, maps = grid8_views
+    i, j = GRID8_PAIRS[u]
+    sx, sy, _ = synth.pair_step(g[i], g[j])
+    p = sva.default_params(D=128, dmin=0, dir=sx, dir_y=sy)
+    disp, _ = ctx.disparity_sgm(views[i], views[j], p)
+    od, _ = oracle.sgm2(views[i], views[j], 128, 0, sx, sy, subpixel=False,
+                        threads=ORACLE_THREADS)
+    assert np.array_equal(disp, od), f"pair {i}->{j} step ({sx},{sy}): " \
+        f"{int((disp != od).sum())} pixels differ"
+    maps[u] = disp
+
+
+def test_config4_grid8_all_fusion(ctx, sva, oracle, grid8_views):
+    """The 7 fused maps of grid8_all (camera i over its pairs (i, j > i)),
+    bit-exact in f64 vs oracle.fuse_depth; maps the per-pair tests did not
+    leave behind are recomputed on the GPU."""
+    g, views, maps = grid8_views
+    n_groups = 0
+    for i in range(7):
+        stack, bases = [], []
+        for u, (a, j) in enumerate(GRID8_PAIRS):
+            if a != i:
+                continue
+            sx, sy, k = synth.pair_step(g[i], g[j])
+            if u not in maps:
+                maps[u], _ = ctx.disparity_sgm(views[i], views[j],
+                                               sva.default_params(D=128, dir=sx, dir_y=sy))
+            stack.append(maps[u])
+            bases.append(k * PITCH)
+        stack = np.ascontiguousarray(np.stack(stack))
+        depth, nv = ctx.fuse_depth(stack, bases, F, PS)
+        exp, en = oracle.fuse_depth(stack, bases, F, PS)
+        assert np.array_equal(nv, en), f"camera {i}"
+        assert np.array_equal(depth.view(np.uint64), exp.view(np.uint64)), f"camera {i}"
+        assert (nv == len(bases)).mean() > 0.3, f"camera {i}"
+        n_groups += 1
+    assert n_groups == 7
 
 
 @pytest.mark.parametrize("kernel", ["cost_volume", "fused"])
