@@ -73,9 +73,6 @@ def parse():
                     help="pairs of a step go round-robin to this many contexts, each with its "
                          "own HIP stream and workspaces, so pairs overlap (0 = auto: 2 when a "
                          "rank has several pairs per step and D != 192, else 1)")
-    ap.add_argument("--path-kernel", default="auto", choices=["auto", "cost_volume", "fused"],
-                    help="sva_set_path_kernel (DESIGN.md §4.5); auto = the library's choice "
-                         "(the cost-volume route)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="gather each step's maps synchronously on the compute stream")
     ap.add_argument("--rehearse-overlap", action="store_true",
@@ -176,10 +173,9 @@ def mode_r_beside(ctx, W, H, rows=24, k=20, reps=3):
 
 def frame_overlap_beside(W, H, D, frames=40, rounds=2):
     """ms per frame for consecutive frames issued round-robin on 1 or 2
-    contexts (each its own stream and workspaces), for both path kernels
-    (sva_set_path_kernel).  The cost-volume kernel is HBM-bound
-    like the WTA after it, so a second stream gains nothing; the fused kernel
-    leaves HBM headroom that the other frame's WTA uses."""
+    contexts (each its own stream and workspaces).  The frame's kernels are
+    HBM-bound, so a second stream gains only the launch gaps and the
+    horizontal-line tail of the path kernel."""
     import torch
     import stereovisionarray_amd as sva
     from stereovisionarray_amd import synth
@@ -208,20 +204,15 @@ def frame_overlap_beside(W, H, D, frames=40, rounds=2):
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / frames * 1e3
 
-    res = {}
-    for name, kern in (("cost_volume", sva.SVA_PATH_KERNEL_COST_VOLUME),
-                       ("fused", sva.SVA_PATH_KERNEL_FUSED)):
-        for c in ctxs:
-            c.set_path_kernel(kern)
-        run(2)
-        best = {}
-        for _ in range(rounds):
-            for n in (1, 2):
-                t = run(n)
-                best[n] = min(best.get(n, t), t)
-        res[name] = {f"{n}_streams": round(best[n], 4) for n in (1, 2)}
+    run(2)
+    best = {}
+    for _ in range(rounds):
+        for n in (1, 2):
+            t = run(n)
+            best[n] = min(best.get(n, t), t)
     for c in ctxs:
         c.close()
+    res = {f"{n}_streams": round(best[n], 4) for n in (1, 2)}
     res["unit"] = "ms/frame"
     res["note"] = (f"{frames} consecutive {W}x{H} D={D} frames round-robin on 1 or 2 contexts "
                    "(own stream + workspaces), best of 2 rounds; not the headline value")
@@ -243,9 +234,8 @@ def load_traffic(workload, kernel="sgm_paths"):
 
 
 # rocprofv3 kernel names -> bench timer names (the PMC pass reports per kernel)
-PMC_KERNELS = {"sgm_paths_kernel": "sgm_paths", "sgm_fused_kernel": "sgm_fused",
-               "wta_h_kernel": "wta_h", "wta_paths_kernel": "wta",
-               "census_cost_kernel": "cost", "census_cost_sweep_kernel": "cost"}
+PMC_KERNELS = {"sgm_paths_kernel": "sgm_paths", "wta_h_kernel": "wta_h",
+               "census_cost_kernel": "cost"}
 
 
 def _pmc_pass(counter, args, outdir):
@@ -282,8 +272,7 @@ def live_traffic(a):
     tallies 128-B streaming reads at 64 B), WRITE_SIZE exact for 16-B stores."""
     import tempfile
     outdir = tempfile.mkdtemp(prefix="sva_pmc_", dir="/tmp")
-    args = ["--workload", a.workload, "--path-kernel", a.path_kernel,
-            "--pairs-per-rank", str(a.pairs_per_rank)]
+    args = ["--workload", a.workload, "--pairs-per-rank", str(a.pairs_per_rank)]
     fetch = _pmc_pass("FETCH_SIZE", args, outdir)
     write = _pmc_pass("WRITE_SIZE", args, outdir)
     out = {}
@@ -374,9 +363,8 @@ def breakdown(a, step, world, ctx, timed_kernels):
     kernels = kernel_table(ctxs)
     for c in ctxs:
         c.set_timing(0)
-    for name in ("sgm_paths", "sgm_fused"):
-        if name in timed_kernels:
-            kernels[name] = timed_kernels[name]
+    if "sgm_paths" in timed_kernels:
+        kernels["sgm_paths"] = timed_kernels["sgm_paths"]
     return kernels
 
 
@@ -434,8 +422,7 @@ def exchange_report(a, step, world, rank, dev, ctxs, last, n_units, ms_per_step,
             "map_bytes_per_unit": int(last[0].numel() * last.element_size())}
 
 
-def kernel_table(ctx, names=("census", "cost", "sgm_paths", "sgm_fused", "wta", "wta_h",
-                              "fuse_depth")):
+def kernel_table(ctx, names=("census", "cost", "sgm_paths", "wta_h", "fuse_depth")):
     """Average hipEvent duration per kernel, pooled over one or several contexts
     (with --streams > 1 the launches overlap, so durations include contention)."""
     ctxs = ctx if isinstance(ctx, list) else [ctx]
@@ -450,24 +437,16 @@ def kernel_table(ctx, names=("census", "cost", "sgm_paths", "sgm_fused", "wta", 
     return kernels
 
 
-# Algorithmic bytes per launch of each path-aggregation kernel:
-#   sgm_paths: SURVEY.md §8(d)'s aggregation model, 10 B/disp (8 u8 C reads + one
-#              u16 S write), whatever the kernel spills;
-#   sgm_fused: forms C in registers, so its own model is the 8 u8 L_r volumes it
-#              writes (8 B/disp) + the two census maps read once (16 B/px).
-PATH_MODELS = {
-    "sgm_paths": (AGG_BYTES_PER_DISP, 0.0, "SURVEY §8d aggregation: 10 B/disp"),
-    "sgm_fused": (8.0, 16.0, "fused: 8 B/disp L_r writes + 16 B/px census reads"),
-}
-
-
+# Algorithmic bytes per launch of the path-aggregation kernel:
+# SURVEY.md §8(d)'s aggregation model, 10 B/disp (8 u8 C reads + one u16 S
+# write), whatever the kernel spills.
 def roofline_of(kernels, W, H, D, workload, overlapped=False):
-    name = "sgm_paths" if "sgm_paths" in kernels else "sgm_fused"
+    name = "sgm_paths"
     agg = kernels.get(name)
     if not agg:
         return None
-    per_disp, per_px, model = PATH_MODELS[name]
-    alg_bytes = per_disp * W * H * D + per_px * W * H
+    model = "SURVEY §8d aggregation: 10 B/disp"
+    alg_bytes = AGG_BYTES_PER_DISP * W * H * D
     achieved = alg_bytes / (agg["avg_ms"] * 1e-3) / 1e9
     out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -753,15 +732,11 @@ def main():
     # (1080p x 256 pairs: 1 stream 251.5K, 2 streams 244.1K Mdisp/s), at D=128
     # and D=256 it gains 4 % / 2 % (profiles/r02_v9/streams_ab.txt).
     n_streams = a.streams if a.streams > 0 else (1 if P == 1 or D == 192 else 2)
-    path_kernel = a.path_kernel
-    kern = {"auto": sva.SVA_PATH_KERNEL_AUTO, "cost_volume": sva.SVA_PATH_KERNEL_COST_VOLUME,
-            "fused": sva.SVA_PATH_KERNEL_FUSED}[path_kernel]
     ctx = sva.Context(local)
     stream = torch.cuda.Stream(dev)     # non-default stream shared by kernels, copies, RCCL
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     ctx.reserve(W, H, D)
-    ctx.set_path_kernel(kern)
     # --streams S: pair j of a step runs on context j % S (own stream and
     # workspaces); the step's maps are complete once `stream` has waited on all
     ctxs, cstreams = [ctx], [stream]
@@ -770,7 +745,6 @@ def main():
         c_ = sva.Context(local)
         c_.set_stream(s_.cuda_stream)
         c_.reserve(W, H, D)
-        c_.set_path_kernel(kern)
         ctxs.append(c_)
         cstreams.append(s_)
 
@@ -879,8 +853,7 @@ def main():
                    "W": W, "H": H, "D": D, "P1": 10, "P2": 120,
                    "parallelism": f"pairs sharded over {world} rank(s), RCCL gather to rank 0"
                                   + (" overlapped with the next step" if nbuf == 2 else ""),
-                   "streams_per_rank": len(ctxs),
-                   "path_kernel": path_kernel if path_kernel != "auto" else "cost_volume"},
+                   "streams_per_rank": len(ctxs)},
         "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
         "roofline": roofline,
         "cpu_baseline": None,

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SVA_ABI_VERSION 3
+#define SVA_ABI_VERSION 4
 
 enum {
     SVA_OK = 0,
@@ -53,7 +53,10 @@ typedef struct sva_camera {
 
 /* Mode S parameters.  Use sva_sgm_params_default(). */
 typedef struct sva_sgm_params {
-    int32_t D;           /* disparity count; GPU path: multiple of 32, 32..256     */
+    int32_t D;           /* disparity count, 1..256 (whole-frame entry points; the
+                            stage entry points take 64, 128, 192 or 256).  Other
+                            D run at the next of those widths with the extra
+                            disparities masked out              */
     int32_t dmin;        /* first disparity                                        */
     int32_t dir;         /* x component of the match step: +1: x+(dmin+d) in the
                             other image, -1: x-(dmin+d) (rectified horizontal);
@@ -97,16 +100,12 @@ const char* sva_status_string(int status);
 /* Pre-size the workspace for W x H x D (optional; calls grow it on demand). */
 int sva_reserve(void* ctx, int width, int height, int D);
 
-/* Path-aggregation kernel for 1-D steps (dir_y = 0) of sva_disparity_sgm*.
- * COST_VOLUME: census -> W*H*D u8 cost volume -> 8-path kernel reading it
- *   (16 B/disp of HBM traffic in the path kernel).
- * FUSED: the path kernel forms the Hamming costs in registers from the census
- *   maps (8 B/disp, no cost volume, more VALU per disparity).
- * AUTO (default): COST_VOLUME.  Since the cost-volume route writes only six
- *   path volumes and recomputes the horizontal paths in its WTA kernel
- *    it is the faster one for every D, on one stream and with
- *   frames overlapping on two.
- * Results are identical.  2-D array steps always use the cost volume. */
+/* Path-aggregation route of sva_disparity_sgm*.  COST_VOLUME (= AUTO, the
+ * default): census -> W*H*D u8 cost volume -> 8-path kernel in checkpoint
+ * mode -> horizontal recompute + WTA.  FUSED (the
+ * census-fused path kernel of ABI v1-v3, slower at every D once the
+ * checkpoint route existed) was removed in ABI v4: selecting it returns
+ * SVA_ERR_UNSUPPORTED. */
 #define SVA_PATH_KERNEL_COST_VOLUME 0
 #define SVA_PATH_KERNEL_FUSED 1
 #define SVA_PATH_KERNEL_AUTO 2
@@ -114,7 +113,7 @@ int sva_set_path_kernel(void* ctx, int kernel);
 
 /* Kernel timing with hipEvents on the context stream (measurement only).
  * enable: SVA_TIMING_OFF, SVA_TIMING_ALL (every launch), or SVA_TIMING_PATHS
- * (only the path-aggregation launch, "sgm_paths" or "sgm_fused": two event records per frame
+ * (only the path-aggregation launch "sgm_paths": two event records per frame
  * instead of eight; each record costs a few microseconds of stream time). */
 #define SVA_TIMING_OFF 0
 #define SVA_TIMING_ALL 1
@@ -149,11 +148,6 @@ int sva_census_cost_d(void* ctx, const uint8_t* left, const uint8_t* right, int 
                       int height, size_t pitch, const sva_sgm_params* p, uint8_t* C);
 int sva_paths_d(void* ctx, const uint8_t* C, int width, int height, const sva_sgm_params* p,
                 uint8_t* L8);
-/* The 8 path volumes straight from the two images through the census-fused
- * path kernel (no cost volume; the kernel sva_disparity_sgm* runs for 1-D
- * steps, dir_y = 0).  Same L8 layout and values as census -> cost -> paths. */
-int sva_paths_fused_d(void* ctx, const uint8_t* left, const uint8_t* right, int width,
-                      int height, size_t pitch, const sva_sgm_params* p, uint8_t* L8);
 int sva_aggregate_d(void* ctx, const uint8_t* C, int width, int height,
                     const sva_sgm_params* p, uint16_t* S);
 /* Checkpoint-mode stages of the cost-volume frame pipeline.

@@ -40,7 +40,7 @@ EXPORTED = [
     "sva_destroy", "sva_set_stream", "sva_synchronize", "sva_last_error",
     "sva_status_string", "sva_reserve", "sva_set_path_kernel", "sva_set_timing", "sva_reset_timing",
     "sva_kernel_time", "sva_disparity_sgm", "sva_disparity_sgm_d", "sva_census_d",
-    "sva_cost_d", "sva_census_cost_d", "sva_paths_d", "sva_paths_fused_d", "sva_aggregate_d", "sva_wta_d", "sva_disparity_ref",
+    "sva_cost_d", "sva_census_cost_d", "sva_paths_d", "sva_aggregate_d", "sva_wta_d", "sva_disparity_ref",
     "sva_disparity_ref_d", "sva_ref_endpoints_d", "sva_disparity_to_depth_d",
     "sva_disparity_to_depth", "sva_fuse_depth_d", "sva_fuse_depth",
     "sva_shift_perspective_d", "sva_shift_perspective", "sva_improve_with_disparity_d",
@@ -150,7 +150,6 @@ def _load() -> ct.CDLL:
         "sva_census_d": (i32, [vp, vp, i32, i32, sz, vp]),
         "sva_cost_d": (i32, [vp, vp, vp, i32, i32, P(SgmParams), vp]),
         "sva_paths_d": (i32, [vp, vp, i32, i32, P(SgmParams), vp]),
-        "sva_paths_fused_d": (i32, [vp, vp, vp, i32, i32, sz, P(SgmParams), vp]),
         "sva_census_cost_d": (i32, [vp, vp, vp, i32, i32, sz, P(SgmParams), vp]),
         "sva_aggregate_d": (i32, [vp, vp, i32, i32, P(SgmParams), vp]),
         "sva_wta_d": (i32, [vp, vp, i32, i32, P(SgmParams), vp, vp]),
@@ -336,10 +335,6 @@ class Context:
     def census_cost_d(self, left, right, W, H, pitch, params, C):
         self._chk(lib.sva_census_cost_d(self.h, _ptr(left), _ptr(right), W, H, pitch,
                                         ct.byref(params), _ptr(C)))
-
-    def paths_fused_d(self, left, right, W, H, pitch, params, L8):
-        self._chk(lib.sva_paths_fused_d(self.h, _ptr(left), _ptr(right), W, H, pitch,
-                                        ct.byref(params), _ptr(L8)))
 
     def aggregate_d(self, C, W, H, params, S):
         self._chk(lib.sva_aggregate_d(self.h, _ptr(C), W, H, ct.byref(params), _ptr(S)))

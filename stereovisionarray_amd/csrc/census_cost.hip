@@ -18,17 +18,16 @@
 //   cost of row y0+p-1         <- words[(p-1) & 1]      (16-byte nt stores)
 //   stage image row y0+p+4     -> ring slot of row y0+p-4 (read by no one now)
 // HBM bytes: 1 B/disparity written + ~1.4 B/pixel of image read.
+// dreal < D (a padded frame): disparities d >= dreal get 255.
 #include "sva_device.h"
 #include "sva_internal.h"
+#include "sva_tuning.h"
 
 namespace sva {
 namespace {
 
 constexpr int CC_BLOCK = 256;
-#ifndef SVA_CC_PXB
-#define SVA_CC_PXB 128
-#endif
-constexpr int PXB = SVA_CC_PXB;      // pixels per workgroup row
+constexpr int PXB = tune::kCensusCostPx;   // pixels per workgroup row
 constexpr int RING = 8;              // image rows in LDS (power of two)
 constexpr int HX = 4, HY = 3;        // half window (9 wide, 7 high)
 constexpr uint64_t kOutsideCC = 1ull << 63;   // never set in a census word (bits 0..61)
@@ -47,7 +46,7 @@ __device__ __forceinline__ uint64_t census_at(const unsigned* const* rows, int s
 template <int NC>
 __global__ __launch_bounds__(CC_BLOCK) void census_cost_kernel(
     const uint8_t* __restrict__ left, const uint8_t* __restrict__ right, int W, int H,
-    size_t pitch, int dmin, int dir, int rows, uint8_t* __restrict__ C) {
+    size_t pitch, int dmin, int dir, int rows, int dreal, uint8_t* __restrict__ C) {
     constexpr int D = NC * 16;
     constexpr int NW = PXB + D - 1;                      // right census words per row
     constexpr int RW = (NW + 8 + 4 + 3) / 4 * 4;         // right ring row bytes (+ dword overrun)
@@ -181,6 +180,10 @@ __global__ __launch_bounds__(CC_BLOCK) void census_cost_kernel(
                             out[q] = ww;
                         }
                     }
+                    if (dreal < D) {                 // padded disparities: cost 255
+#pragma unroll
+                        for (int q = 0; q < 4; q++) out[q] |= pad_bytes(16 * c + 4 * q, dreal);
+                    }
                     store16_nt(C + ((size_t)y * W + x) * D + 16 * c, out);
                 }
             }
@@ -198,21 +201,18 @@ __global__ __launch_bounds__(CC_BLOCK) void census_cost_kernel(
 bool census_cost_supported(int D) { return D == 64 || D == 128 || D == 192 || D == 256; }
 
 hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right, int W, int H,
-                              size_t pitch, int D, int dmin, int dir, uint8_t* C) {
+                              size_t pitch, int D, int dmin, int dir, uint8_t* C, int dreal) {
+    if (dreal <= 0) dreal = D;
     ScopedKernelTimer t(c, "cost");
-#ifdef SVA_CC_ROWS   // A/B builds only
-    const int rows = SVA_CC_ROWS;
-#else
-    const int rows = 4;   // measured 1080p D=64/128/192, rows 2/4/8/16: 4 best
-#endif
+    const int rows = tune::kCensusCostRows;
     const int bpr = (W + PXB - 1) / PXB;
     const dim3 grid((unsigned)(bpr * ((H + rows - 1) / rows)));
     const int sd = dir > 0 ? 1 : -1;
     switch (D) {
-        case 64: hipLaunchKernelGGL(census_cost_kernel<4>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, C); break;
-        case 128: hipLaunchKernelGGL(census_cost_kernel<8>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, C); break;
-        case 192: hipLaunchKernelGGL(census_cost_kernel<12>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, C); break;
-        case 256: hipLaunchKernelGGL(census_cost_kernel<16>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, C); break;
+        case 64: hipLaunchKernelGGL(census_cost_kernel<4>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
+        case 128: hipLaunchKernelGGL(census_cost_kernel<8>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
+        case 192: hipLaunchKernelGGL(census_cost_kernel<12>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
+        case 256: hipLaunchKernelGGL(census_cost_kernel<16>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

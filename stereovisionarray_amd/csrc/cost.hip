@@ -1,12 +1,10 @@
 // cost.hip -- Hamming matching-cost volume.
 //
-// C[(y*W + x)*D + d] = popcount(CL(x,y) ^ CR(x + dir*(dmin+d), y)), 62 outside.
-// A 256-thread workgroup owns PX = 4096/D consecutive pixels of one row; the
-// right-census words they touch (PX + D - 1 of them) are staged once in LDS.
-// Each thread produces 16 disparities = one 16-byte store, so a wave writes
-// 1 KiB contiguous.  HBM bytes: 1 B/disparity written + 16 B/pixel read.
-#include <cstdlib>
-
+// C[(y*W + x)*D + d] = popcount(CL(x,y) ^ CR(x + dir*(dmin+d), y)), 62 outside,
+// from two census maps: the 1-D kernel (hamming_cost_rows_kernel, below) and
+// the 2-D array-step kernel (hamming_cost2_kernel).  Each thread produces 16
+// disparities = one 16-byte store.  HBM bytes: 1 B/disparity written +
+// 16 B/pixel read.
 #include "sva_device.h"
 #include "sva_internal.h"
 
@@ -21,69 +19,12 @@ constexpr int BLOCK = 256;
 // build listed twice gave temporal 1.155/1.172 ms vs nt 1.169/1.142 ms per
 // full frame (a first, single-listing A/B had suggested -3.8 %).
 __device__ __forceinline__ void store_cost_nt(uint8_t* p, const unsigned (&o)[4]) {
-#ifdef SVA_COST_TEMPORAL   // A/B switch
-    *(uint4*)p = make_uint4(o[0], o[1], o[2], o[3]);
-#else
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store((v4u){o[0], o[1], o[2], o[3]}, (v4u*)p);
-#endif
 }
 
 // Out-of-image marker: bit 63 is never set in a census word (bits 0..61).
 constexpr uint64_t kOutside = 1ull << 63;
-constexpr int MAXW = 4096 / 64 + 256;  // LDS words for the smallest D (64): PX=64, +D
-
-// LDS word swizzle.  The D/16 lanes of one pixel read words 16 apart (one per
-// 16-disparity chunk): unswizzled that is a 4-way ds_read_b64 bank conflict at
-// D=128.  XOR-ing bits 0-2 of the word index with bits 4-6 (the chunk) spreads
-// the chunks of a pixel over 8 different bank pairs.  Bijective within each
-// aligned 128-word block, so MAXW rounded up to 128 words is enough.
-__device__ __forceinline__ int swz(int j) { return j ^ ((j >> 4) & 7); }
-
-__global__ __launch_bounds__(BLOCK) void hamming_cost_kernel(const uint64_t* __restrict__ cl,
-                                                              const uint64_t* __restrict__ cr,
-                                                              int W, int H, int D, int dmin,
-                                                              int dir, uint8_t* __restrict__ C) {
-    __shared__ uint64_t rw[(MAXW + 127) / 128 * 128];
-    __shared__ uint8_t rvalid[MAXW];
-    const int tpp = D / 16;                  // threads per pixel
-    const int px_per_block = BLOCK / tpp;    // pixels per block
-    const int blocks_per_row = (W + px_per_block - 1) / px_per_block;
-    const int y = blockIdx.x / blocks_per_row;
-    const int x0 = (blockIdx.x - y * blocks_per_row) * px_per_block;
-    // Right-census range touched by pixels [x0, x0+px) and d in [0, D):
-    // column = x + dir*(dmin + d).  Index LDS by j = (x - x0) + d, column =
-    // x0 + dir*dmin + (dir>0 ? j : ...) -- handled below for both signs.
-    const int nwords = px_per_block + D - 1;
-    for (int j = threadIdx.x; j < nwords; j += BLOCK) {
-        // dir = +1: word j <-> column x0 + dmin + j          (x - x0) + d = j
-        // dir = -1: word j <-> column x0 + px - 1 - dmin - j  (px-1-(x-x0)) + d = j
-        int col = dir > 0 ? x0 + dmin + j : x0 + px_per_block - 1 - dmin - j;
-        bool ok = col >= 0 && col < W;
-        rw[swz(j)] = ok ? cr[(size_t)y * W + col] : 0ull;
-        rvalid[j] = ok;
-    }
-    __syncthreads();
-    const int lp = threadIdx.x / tpp;        // pixel within block
-    const int x = x0 + lp;
-    if (lp >= px_per_block || x >= W) return;  // D=192: 256 % 12 != 0 leaves idle lanes
-    const int d0 = (threadIdx.x - lp * tpp) * 16;
-    const uint64_t l = cl[(size_t)y * W + x];
-    unsigned out[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        unsigned w = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const int d = d0 + q * 4 + b;
-            const int j = dir > 0 ? lp + d : (px_per_block - 1 - lp) + d;
-            unsigned cst = rvalid[j] ? (unsigned)__popcll(l ^ rw[swz(j)]) : 62u;
-            w |= cst << (8 * b);
-        }
-        out[q] = w;
-    }
-    *(uint4*)(C + ((size_t)y * W + x) * D + d0) = make_uint4(out[0], out[1], out[2], out[3]);
-}
 
 // 2-D matching step: the word for (x, y, d) sits at
 // q + off(s), off = step_offset(., bx, by), s = dmin + d, by != 0 (vertical,
@@ -111,7 +52,7 @@ constexpr int kCost2LdsBytes = 64 * 1024;
 template <int NC>
 __global__ __launch_bounds__(BLOCK) void hamming_cost2_kernel(
     const uint64_t* __restrict__ cl, const uint64_t* __restrict__ cr, int W, int H, int dmin,
-    int bx, int by, int R, int T, int ncolb, int bmin, uint8_t* __restrict__ C) {
+    int bx, int by, int R, int T, int ncolb, int bmin, int dreal, uint8_t* __restrict__ C) {
     constexpr int D = NC * 16, PX = BLOCK / NC, G = 32 / NC > 0 ? 32 / NC : 1;
     extern __shared__ uint64_t smem[];
     uint64_t* rw = smem;                       // [T][PX] census words
@@ -154,6 +95,10 @@ __global__ __launch_bounds__(BLOCK) void hamming_cost2_kernel(
             }
             out[q] = w;
         }
+        if (dreal < D) {                             // padded disparities: cost 255
+#pragma unroll
+            for (int q = 0; q < 4; q++) out[q] |= pad_bytes(16 * c + 4 * q, dreal);
+        }
         store_cost_nt(C + ((size_t)y * W + x) * D + c * 16, out);
     }
 }
@@ -188,7 +133,7 @@ __host__ __device__ constexpr int cost_rows(int W, int H, int D) {
 template <int NC>
 __global__ __launch_bounds__(256) void hamming_cost_rows_kernel(
     const uint64_t* __restrict__ cl, const uint64_t* __restrict__ cr, int W, int H, int dmin,
-    int dir, int rows, uint8_t* __restrict__ C) {
+    int dir, int rows, int dreal, uint8_t* __restrict__ C) {
     constexpr int D = NC * 16, NT = (256 / (16 * NC) > 0 ? 256 / (16 * NC) : 1) * 16 * NC;
     constexpr int PX = NT / NC, NW = PX + D - 1;
     constexpr int WPT = (NW + NT - 1) / NT;  // staged words per thread
@@ -253,6 +198,10 @@ __global__ __launch_bounds__(256) void hamming_cost_rows_kernel(
                     out[q] = ww;
                 }
             }
+            if (dreal < D) {                         // padded disparities: cost 255
+#pragma unroll
+                for (int q = 0; q < 4; q++) out[q] |= pad_bytes(16 * c + 4 * q, dreal);
+            }
             store_cost_nt(C + ((size_t)y * W + x) * D + 16 * c, out);
         }
     }
@@ -261,8 +210,9 @@ __global__ __launch_bounds__(256) void hamming_cost_rows_kernel(
 }  // namespace
 
 hipError_t launch_cost2(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,
-                        int dmin, int sx, int sy, uint8_t* C) {
-    if (sy == 0) return launch_cost(c, cl, cr, W, H, D, dmin, sx > 0 ? 1 : -1, C);
+                        int dmin, int sx, int sy, uint8_t* C, int dreal) {
+    if (dreal <= 0) dreal = D;
+    if (sy == 0) return launch_cost(c, cl, cr, W, H, D, dmin, sx > 0 ? 1 : -1, C, dreal);
     ScopedKernelTimer t(c, "cost");
     // reduce the step to its primitive lattice vector (same offsets, more reuse)
     int a = sx < 0 ? -sx : sx, b = sy < 0 ? -sy : sy;
@@ -283,7 +233,7 @@ hipError_t launch_cost2(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, i
     const size_t lds = (size_t)T * px * 8 + (size_t)T * 8;
 #define SVA_COST2(NC)                                                                          \
     hipLaunchKernelGGL(hamming_cost2_kernel<NC>, grid, dim3(BLOCK), lds, c.stream, cl, cr, W, H, \
-                       dmin, bx, by, R, T, ncolb, bmin, C)
+                       dmin, bx, by, R, T, ncolb, bmin, dreal, C)
     switch (nc) {
         case 4: SVA_COST2(4); break;
         case 8: SVA_COST2(8); break;
@@ -296,35 +246,21 @@ hipError_t launch_cost2(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, i
 }
 
 hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,
-                       int dmin, int dir, uint8_t* C) {
+                       int dmin, int dir, uint8_t* C, int dreal) {
+    if (dreal <= 0) dreal = D;
     ScopedKernelTimer t(c, "cost");
-    const int px_per_block = BLOCK / (D / 16);
-    const int blocks_per_row = (W + px_per_block - 1) / px_per_block;
-#ifdef SVA_PATHS_ABLATION   // A/B builds only: SVA_COST_VARIANT=1 selects the single-row kernel
-    static const int variant = getenv("SVA_COST_VARIANT") ? atoi(getenv("SVA_COST_VARIANT")) : 0;
-#else
-    constexpr int variant = 0;
-#endif
-    if (variant == 1 || (D != 64 && D != 128 && D != 192 && D != 256)) {  // single-row kernel
-        hipLaunchKernelGGL(hamming_cost_kernel, dim3(blocks_per_row * H), dim3(BLOCK), 0,
-                           c.stream, cl, cr, W, H, D, dmin, dir, C);
-        return hipGetLastError();
-    }
-#ifdef SVA_COST_ROWS   // A/B builds only
-    const int rows = SVA_COST_ROWS;
-#else
     const int rows = cost_rows(W, H, D);
-#endif
     // threads: 16 pixels x NC chunks per group, as many groups as fit 256
     const int nc = D / 16, groups = 256 / (16 * nc) > 0 ? 256 / (16 * nc) : 1;
     const int nt = groups * 16 * nc, px = groups * 16;
     const int bpr = (W + px - 1) / px;
     const dim3 grid((unsigned)(bpr * ((H + rows - 1) / rows)));
     switch (D) {
-        case 64: hipLaunchKernelGGL(hamming_cost_rows_kernel<4>, grid, dim3(nt), 0, c.stream, cl, cr, W, H, dmin, dir, rows, C); break;
-        case 128: hipLaunchKernelGGL(hamming_cost_rows_kernel<8>, grid, dim3(nt), 0, c.stream, cl, cr, W, H, dmin, dir, rows, C); break;
-        case 192: hipLaunchKernelGGL(hamming_cost_rows_kernel<12>, grid, dim3(nt), 0, c.stream, cl, cr, W, H, dmin, dir, rows, C); break;
-        case 256: hipLaunchKernelGGL(hamming_cost_rows_kernel<16>, grid, dim3(nt), 0, c.stream, cl, cr, W, H, dmin, dir, rows, C); break;
+        case 64: hipLaunchKernelGGL(hamming_cost_rows_kernel<4>, grid, dim3(nt), 0, c.stream, cl, cr, W, H, dmin, dir, rows, dreal, C); break;
+        case 128: hipLaunchKernelGGL(hamming_cost_rows_kernel<8>, grid, dim3(nt), 0, c.stream, cl, cr, W, H, dmin, dir, rows, dreal, C); break;
+        case 192: hipLaunchKernelGGL(hamming_cost_rows_kernel<12>, grid, dim3(nt), 0, c.stream, cl, cr, W, H, dmin, dir, rows, dreal, C); break;
+        case 256: hipLaunchKernelGGL(hamming_cost_rows_kernel<16>, grid, dim3(nt), 0, c.stream, cl, cr, W, H, dmin, dir, rows, dreal, C); break;
+        default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }

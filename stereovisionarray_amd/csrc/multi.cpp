@@ -297,7 +297,7 @@ int run_pairs(Multi* m, const Plan& P, const std::vector<const uint8_t*>& left,
 }
 
 int check_params(const sva_sgm_params& p) {
-    if (!paths_supported(p.D) || p.dmin < 0 || (p.dir == 0 && p.dir_y == 0))
+    if (!padded_D(p.D) || p.dmin < 0 || (p.dir == 0 && p.dir_y == 0))
         return SVA_ERR_INVALID_ARG;
     return SVA_OK;
 }

@@ -17,6 +17,7 @@
 
 #include "sva_device.h"
 #include "sva_internal.h"
+#include "sva_tuning.h"
 
 namespace sva {
 namespace {
@@ -235,14 +236,8 @@ __device__ __forceinline__ unsigned scan64_dpp(unsigned v) {
 constexpr int P3_ROWS = 32;                          // 4 waves x 8 rows
 constexpr int P3_RW_MAX = 63 + 2 * PT_MAXK;          // region columns
 constexpr int P3_RS = 100;                           // R column stride: 25 dwords (odd)
-#ifndef SVA_P3_OU_KB
-#define SVA_P3_OU_KB 24
-#endif
-#ifndef SVA_P3_WORDS
-#define SVA_P3_WORDS 1024
-#endif
-constexpr int P3_OU_BYTES = SVA_P3_OU_KB * 1024;     // staged O chunk
-constexpr int P3_WORDS = SVA_P3_WORDS;               // offset bitmap per pass: 32K bits
+constexpr int P3_OU_BYTES = tune::kPlaneOuKB * 1024;  // staged O chunk
+constexpr int P3_WORDS = tune::kPlaneWords;            // offset bitmap per pass: 32K bits
 constexpr int P3_MAX_OUT = 1024;                     // outer offsets per pass
 
 // Interval [lo, lo + len) of inner offsets d_in on a pixel's line at outer
@@ -290,11 +285,8 @@ __device__ __forceinline__ void line_interval(int po, int pa, int pn, bool mi, b
     }
 }
 
-#ifndef SVA_P3_MINB
-#define SVA_P3_MINB 3
-#endif
 template <int K>
-__global__ __launch_bounds__(256, SVA_P3_MINB) void ref_plane3_kernel(
+__global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     const uint8_t* __restrict__ ref, const uint8_t* __restrict__ other, int W, int H, size_t pitch,
     const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
     const uint8_t* __restrict__ valid_in, uint8_t* __restrict__ disp_u8,

@@ -1,12 +1,13 @@
-// sgm_common.h -- device pieces shared by the two 8-path aggregation kernels
-// (sgm_paths.hip reads a materialised cost volume; sgm_fused.hip computes the
-// Hamming costs from the census maps on the fly).  DESIGN.md §4.3 / §4.5.
+// sgm_common.h -- device pieces of the 8-path aggregation shared by the path
+// kernel (sgm_paths.hip) and the horizontal recompute + WTA kernel
+// (wta_h.hip).  DESIGN.md §4.3 / §4.6.
 #pragma once
 
 #include <utility>
 
 #include "sva_device.h"
 #include "sva_internal.h"
+#include "sva_tuning.h"
 
 namespace sva {
 namespace sgm {
@@ -68,12 +69,8 @@ struct Words {
     unsigned w[NW];
 };
 
-// Cache-policy bits of the C loads.  A/B (full frame, in-process): nt (2)
-// +8 %, sc0+nt (3) +8 %; sc0 (1), sc0+sc1 (17), 8, 16 within the +-2 % noise.
-#ifndef SVA_C_LOAD_AUX
-#define SVA_C_LOAD_AUX 0
-#endif
-template <int NW, int AUX = SVA_C_LOAD_AUX>
+// Cache-policy bits of the C loads (tune::kCLoadAux).
+template <int NW, int AUX = tune::kCLoadAux>
 __device__ __forceinline__ Words<NW> bload(rsrc_t r, unsigned off) {
     Words<NW> o;
     if constexpr (NW == 1) {
@@ -91,15 +88,10 @@ __device__ __forceinline__ Words<NW> bload(rsrc_t r, unsigned off) {
     return o;
 }
 
-// VAR (experiment builds only, csrc/experiments/): 2 = no stores,
-// 3 = no loads, 4 = neither.  Production code is VAR = 0.  AUX = cache-policy
-// bits of the store (kStoreNT for the streamed L_r volumes).
-template <int NW, int VAR, int AUX = kStoreNT>
+// AUX = cache-policy bits of the store (kStoreNT for the streamed L_r volumes).
+template <int NW, int AUX = kStoreNT>
 __device__ __forceinline__ void bstore(rsrc_t r, unsigned off, const unsigned (&w)[NW]) {
-    if constexpr (VAR == 2 || VAR == 4) {
-#pragma unroll
-        for (int i = 0; i < NW; i++) asm volatile("" ::"v"(w[i]));
-    } else if constexpr (NW == 1) {
+    if constexpr (NW == 1) {
         __builtin_amdgcn_raw_buffer_store_b32(w[0], r, off, 0, AUX);
     } else if constexpr (NW == 2) {
         typedef unsigned v2u __attribute__((ext_vector_type(2)));
@@ -247,57 +239,20 @@ __device__ __forceinline__ void dir_of(int r, int& rx, int& ry) {
     ry = T[r][1];
 }
 
-// Prefetch depth in steps, per line kind.  Horizontal lines are the longest
-// (W steps) and few (2H lines): once the vertical/diagonal lines drain they
-// run alone and latency-bound, so they get a deeper ring (their next steps
-// are contiguous bytes, and VGPRs are not what limits occupancy here: the
-// grid has ~3.3 waves per SIMD at 1080p).
-// Measured in-process A/B (tools/ab_paths.py, 1080p D=128, same buffers,
-// alternating builds): PF_H/PF_V 8/8 0.755-0.788 ms; 32/8 0.665; 32/12 0.661;
-// 28/8 0.664; 40/8 0.689 (181 VGPRs -> 2 waves/SIMD); 32/4 0.770.  Part of the
-// gain is the occupancy cap itself: 149 VGPRs -> 3 waves/SIMD, and 8/8 with
-// LDS forcing 3 workgroups/CU is 0.730 vs 0.788 -- fewer concurrent line
-// streams, better DRAM locality.
-// Per disparities-per-lane (D = 16*DPL) overrides: SVA_PF_H<DPL>/SVA_PF_V<DPL>.
-// Chosen by the same in-process A/B: D=64 (1080p) 40/12 0.372 ms vs 8/8 0.416;
-// D=192 24/8 0.996 vs 12/8 1.154; D=256 (4K) 12/8 stays best (16/8 equal,
-// 20/8 and 12/12 +3 %).
-#ifndef SVA_PF_H4
-#define SVA_PF_H4 40
-#endif
-#ifndef SVA_PF_V4
-#define SVA_PF_V4 12
-#endif
-#ifndef SVA_PF_H8
-#define SVA_PF_H8 32
-#endif
-#ifndef SVA_PF_V8
-#define SVA_PF_V8 12
-#endif
-#ifndef SVA_PF_H12
-#define SVA_PF_H12 24
-#endif
-#ifndef SVA_PF_V12
-#define SVA_PF_V12 8
-#endif
-#ifndef SVA_PF_H16
-#define SVA_PF_H16 12
-#endif
-#ifndef SVA_PF_V16
-#define SVA_PF_V16 8
-#endif
+// Prefetch depth in steps, per line kind (tune::kPf*, with the A/B that
+// chose each value).
 template <int DPL> constexpr int pf_h() {
-    return DPL == 4 ? SVA_PF_H4 : DPL == 8 ? SVA_PF_H8 : DPL == 12 ? SVA_PF_H12 : SVA_PF_H16;
+    return DPL == 4 ? tune::kPfH4 : DPL == 8 ? tune::kPfH8 : DPL == 12 ? tune::kPfH12 : tune::kPfH16;
 }
 template <int DPL> constexpr int pf_v() {
-    return DPL == 4 ? SVA_PF_V4 : DPL == 8 ? SVA_PF_V8 : DPL == 12 ? SVA_PF_V12 : SVA_PF_V16;
+    return DPL == 4 ? tune::kPfV4 : DPL == 8 ? tune::kPfV8 : DPL == 12 ? tune::kPfV12 : tune::kPfV16;
 }
 
 
 // One path line over a materialised cost volume C.  CKPT
 // (horizontal lines only): store segment checkpoints to rCK instead of the
 // full L_r line to rL.
-template <int DPL, bool DIAG, int VAR, int PF, bool CKPT = false>
+template <int DPL, bool DIAG, int PF, bool CKPT = false>
 __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& g, int rx, int ry,
                                           int line, int k, rsrc_t rCK) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
@@ -343,12 +298,7 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
     Words<NW> ring[PF];
 #pragma unroll
     for (int p = 0; p < PF; p++) {
-        if constexpr (VAR == 3 || VAR == 4) {
-#pragma unroll
-            for (int w = 0; w < NW; w++) ring[p].w[w] = (0x05030201u * (unsigned)(p + 1) + (unsigned)k) & 0x1f1f1f1fu;
-        } else {
-            ring[p] = bload<NW>(rC, pc.off);
-        }
+        ring[p] = bload<NW>(rC, pc.off);
         pc.off += stride;
         if constexpr (DIAG) {   // the advance past pixel PF-1 is checked by step 0
             if (p < PF - 1) {
@@ -381,10 +331,10 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
             const bool hit = rx > 0 ? (((x + 1) & (SEG - 1)) == 0 && x + 1 < W)
                                     : ((x & (SEG - 1)) == 0 && x > 0);
             if (hit)   // default policy: the WTA kernel reads these back soon
-                bstore<NW, VAR, 0>(rCK, ((unsigned)(y0 * g.ns + (x >> SL)) * (unsigned)D +
+                bstore<NW, 0>(rCK, ((unsigned)(y0 * g.ns + (x >> SL)) * (unsigned)D +
                                          (unsigned)(k * DPL)), ow);
         } else {
-            bstore<NW, VAR>(rL, cc.off, ow);
+            bstore<NW>(rL, cc.off, ow);
         }
         cc.off += stride;
         if constexpr (DIAG) {
@@ -418,12 +368,7 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
         }
         if (refill) {
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (VAR == 3 || VAR == 4) {
-#pragma unroll
-                for (int w = 0; w < NW; w++) ring[p].w[w] = (cw[w] * 3u + (unsigned)p) & 0x1f1f1f1fu;
-            } else {
-                ring[p] = bload<NW>(rC, pc.off);
-            }
+            ring[p] = bload<NW>(rC, pc.off);
             pc.off += stride;                // wrap corrected by the next step
             __builtin_amdgcn_sched_barrier(0);
         }

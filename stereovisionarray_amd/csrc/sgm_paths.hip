@@ -68,16 +68,16 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
     const int slot = g.ckpt ? r - 2 : r;
     if (r >= 4) {
         const rsrc_t rL = make_rsrc(L8 + (size_t)slot * g.vol, g.vol);
-        path_line<DPL, true, 0, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
+        path_line<DPL, true, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
     } else if (r >= 2) {
         const rsrc_t rL = make_rsrc(L8 + (size_t)slot * g.vol, g.vol);
-        path_line<DPL, false, 0, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
+        path_line<DPL, false, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
     } else if (g.ckpt) {
         const rsrc_t rCK = make_rsrc(CK + (size_t)r * g.ckvol, g.ckvol);
-        path_line<DPL, false, 0, pf_h<DPL>(), true>(rC, rC, g, rx, ry, line, k, rCK);
+        path_line<DPL, false, pf_h<DPL>(), true>(rC, rC, g, rx, ry, line, k, rCK);
     } else {
         const rsrc_t rL = make_rsrc(L8 + (size_t)r * g.vol, g.vol);
-        path_line<DPL, false, 0, pf_h<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
+        path_line<DPL, false, pf_h<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
     }
 }
 

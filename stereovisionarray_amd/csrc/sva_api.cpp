@@ -138,11 +138,17 @@ int check_image(Ctx* c, const void* a, int W, int H, size_t pitch) {
 // Shape limits are checked here, before any workspace is allocated: kernels
 // launch with gridDim.y = H (lr_check, refine's gathers), which caps H at
 // 65535, and every path volume is addressed with 32-bit buffer offsets.
-int check_sgm(Ctx* c, const sva_sgm_params* p, int W, int H) {
+// Whole-frame entry points take any D in 1..256 (run at the padded native
+// width); the stage entry points (native = true) read and
+// write [..][D] volumes and take D in {64, 128, 192, 256}.
+int check_sgm(Ctx* c, const sva_sgm_params* p, int W, int H, bool native = false) {
     if (!p) return fail(c, SVA_ERR_INVALID_ARG, "null params");
     if (p->D <= 0) return fail(c, SVA_ERR_INVALID_ARG, "D must be positive");
-    if (!paths_supported(p->D))
-        return fail(c, SVA_ERR_UNSUPPORTED, "GPU path built for D in {64,128,192,256}");
+    const int Dp = padded_D(p->D);
+    if (!Dp) return fail(c, SVA_ERR_UNSUPPORTED, "GPU path built for D in 1..256");
+    if (native && !paths_supported(p->D))
+        return fail(c, SVA_ERR_UNSUPPORTED,
+                    "stage entry points take D in {64,128,192,256} (whole frames: any D <= 256)");
     if (p->dir < -255 || p->dir > 255 || p->dir_y < -255 || p->dir_y > 255 ||
         (p->dir == 0 && p->dir_y == 0))
         return fail(c, SVA_ERR_INVALID_ARG, "(dir, dir_y) must be a nonzero step, |comp| <= 255");
@@ -154,64 +160,9 @@ int check_sgm(Ctx* c, const sva_sgm_params* p, int W, int H) {
     if (p->lr_check && p->lr_max_diff < 0)
         return fail(c, SVA_ERR_INVALID_ARG, "lr_max_diff must be >= 0");
     if (H > 65535) return fail(c, SVA_ERR_UNSUPPORTED, "H must be <= 65535");
-    if (W > 0 && H > 0 && (unsigned long long)W * (unsigned long long)H * (unsigned)p->D >=
+    if (W > 0 && H > 0 && (unsigned long long)W * (unsigned long long)H * (unsigned)Dp >=
                               (1ull << 32))
         return fail(c, SVA_ERR_UNSUPPORTED, "W*H*D must be < 2^32 (32-bit volume offsets)");
-    return SVA_OK;
-}
-
-// Path kernel selection (sva_set_path_kernel): the census-fused
-// kernel serves 1-D steps (dir_y = 0); array pairs on 2-D steps always use the
-// materialised cost volume (cost2 + sgm_paths).
-bool use_fused(const Ctx* c, const sva_sgm_params* p, int W, int H) {
-    // AUTO = the cost-volume route for every D
-    const bool want = c->path_kernel == SVA_PATH_KERNEL_FUSED;
-    return want && p->dir_y == 0 && fused_fits(W, H, p->D, p->dmin);
-}
-
-// Padded census pair for the fused path: one buffer [Lp | Rp], each map
-// H rows of W + pr words.  Returns the map size in words.
-int census_padded(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int H, size_t pitch,
-                  const sva_sgm_params* p, size_t* map_words) {
-    const int pr = fused_pad(W, p->D, p->dmin);
-    const size_t mw = (size_t)H * (size_t)(W + pr);
-    SVA_HIP(c, c->census_l.ensure(2 * mw * 8), "census workspace");
-    uint64_t* cen = (uint64_t*)c->census_l.ptr;
-    SVA_HIP(c, launch_census_pair_padded(*c, left, right, W, H, pitch, pr, cen, cen + mw),
-            "census launch");
-    *map_words = mw;
-    return SVA_OK;
-}
-
-// The fused path kernel for one reference/matched role of the padded census pair.
-int fused_paths(Ctx* c, size_t mw, bool swap, int W, int H, const sva_sgm_params* p, int dir,
-                uint8_t* L8) {
-    SVA_HIP(c, launch_paths_fused(*c, (const uint64_t*)c->census_l.ptr, 2 * mw, swap ? mw : 0,
-                                  swap ? 0 : mw, W, H, p->D, p->dmin, dir, p->P1, p->P2, L8),
-            "paths launch");
-    return SVA_OK;
-}
-
-int run_sgm_fused(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int H, size_t pitch,
-                  const sva_sgm_params* p, uint16_t* disp, float* sub) {
-    const size_t np = (size_t)W * H, nv = np * (size_t)p->D;
-    const int dir = p->dir > 0 ? 1 : -1;
-    SVA_HIP(c, c->paths.ensure(nv * 8), "path workspace");
-    uint8_t* L8 = (uint8_t*)c->paths.ptr;
-    size_t mw = 0;
-    int s = census_padded(c, left, right, W, H, pitch, p, &mw);
-    if (s) return s;
-    if ((s = fused_paths(c, mw, false, W, H, p, dir, L8))) return s;
-    SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, disp, sub), "wta launch");
-    if (p->lr_check) {
-        SVA_HIP(c, c->disp_r.ensure(np * 2), "lr workspace");
-        uint16_t* dr = (uint16_t*)c->disp_r.ptr;
-        // right image as reference: the census maps swap roles, the step flips
-        if ((s = fused_paths(c, mw, true, W, H, p, -dir, L8))) return s;
-        SVA_HIP(c, launch_wta_from_paths(*c, L8, W, H, p->D, p->dmin, dr, nullptr), "wta launch");
-        SVA_HIP(c, launch_lr_check(*c, disp, dr, sub, W, H, dir, 0, p->lr_max_diff, p->invalid),
-                "lr launch");
-    }
     return SVA_OK;
 }
 
@@ -219,25 +170,28 @@ size_t ckpt_bytes(int W, int H, int D) { return 2 * (size_t)H * ckpt_segments(W,
 
 // Paths + WTA of the cost-volume frame pipeline: sgm_paths
 // in checkpoint mode (6 volumes + horizontal checkpoints), then wta_h, which
-// recomputes the two horizontal directions per segment and picks d*.
-int paths_wta(Ctx* c, const uint8_t* C, int W, int H, const sva_sgm_params* p, uint16_t* disp,
-              float* sub) {
-    const size_t nv = (size_t)W * H * (size_t)p->D;
+// recomputes the two horizontal directions per segment and picks d*.  Dp is
+// the native volume width, p->D <= Dp the caller's disparities (§4.7).
+int paths_wta(Ctx* c, const uint8_t* C, int W, int H, const sva_sgm_params* p, int Dp,
+              uint16_t* disp, float* sub) {
+    const size_t nv = (size_t)W * H * (size_t)Dp;
     SVA_HIP(c, c->paths.ensure(nv * 6), "path workspace");
-    SVA_HIP(c, c->ckpt.ensure(ckpt_bytes(W, H, p->D)), "checkpoint workspace");
+    SVA_HIP(c, c->ckpt.ensure(ckpt_bytes(W, H, Dp)), "checkpoint workspace");
     uint8_t* L6 = (uint8_t*)c->paths.ptr;
     uint8_t* CK = (uint8_t*)c->ckpt.ptr;
-    SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L6, CK), "paths launch");
-    SVA_HIP(c, launch_wta_h(*c, C, L6, CK, W, H, p->D, p->P1, p->P2, p->dmin, disp, sub),
+    SVA_HIP(c, launch_paths(*c, C, W, H, Dp, p->P1, p->P2, L6, CK), "paths launch");
+    SVA_HIP(c, launch_wta_h(*c, C, L6, CK, W, H, Dp, p->P1, p->P2, p->dmin, disp, sub, p->D),
             "wta launch");
     return SVA_OK;
 }
 
 // Mode S on device buffers: census -> cost -> 8 paths -> WTA (-> L/R check).
+// Any D in 1..256 runs at the native width Dp = padded_D(D): the cost kernels
+// write 255 at d >= D and the WTA ignores those disparities.
 int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int H, size_t pitch,
                    const sva_sgm_params* p, uint16_t* disp, float* sub) {
-    if (use_fused(c, p, W, H)) return run_sgm_fused(c, left, right, W, H, pitch, p, disp, sub);
-    const size_t np = (size_t)W * H, nv = np * (size_t)p->D;
+    const int Dp = padded_D(p->D);
+    const size_t np = (size_t)W * H, nv = np * (size_t)Dp;
     int s;
     SVA_HIP(c, c->cost.ensure(nv), "cost workspace");
     uint8_t* C = (uint8_t*)c->cost.ptr;
@@ -246,19 +200,20 @@ int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int
         SVA_HIP(c, c->disp_r.ensure(np * 2), "lr workspace");
         dr = (uint16_t*)c->disp_r.ptr;
     }
-    if (p->dir_y == 0 && p->D >= 128 && census_cost_supported(p->D) && !c->split_census) {
+    if (p->dir_y == 0 && Dp >= 128 && census_cost_supported(Dp)) {
         // census maps stay on chip: one census+cost kernel (census_cost.hip),
         // once per matching role when the L/R check runs.
         // In-process A/B per frame at 1080p: D=128 1.129 -> 1.112 ms,
         // D=192 1.646 -> 1.588 ms; D=64 is faster split (0.609 vs 0.650 ms).
-        SVA_HIP(c, launch_census_cost(*c, left, right, W, H, pitch, p->D, p->dmin, p->dir, C),
+        SVA_HIP(c, launch_census_cost(*c, left, right, W, H, pitch, Dp, p->dmin, p->dir, C, p->D),
                 "cost launch");
-        if ((s = paths_wta(c, C, W, H, p, disp, sub))) return s;
+        if ((s = paths_wta(c, C, W, H, p, Dp, disp, sub))) return s;
         if (p->lr_check) {
             // right image as reference: the images swap roles, the step flips
-            SVA_HIP(c, launch_census_cost(*c, right, left, W, H, pitch, p->D, p->dmin, -p->dir, C),
+            SVA_HIP(c, launch_census_cost(*c, right, left, W, H, pitch, Dp, p->dmin, -p->dir, C,
+                                          p->D),
                     "cost launch");
-            if ((s = paths_wta(c, C, W, H, p, dr, nullptr))) return s;
+            if ((s = paths_wta(c, C, W, H, p, Dp, dr, nullptr))) return s;
             SVA_HIP(c, launch_lr_check(*c, disp, dr, sub, W, H, p->dir, 0, p->lr_max_diff,
                                        p->invalid),
                     "lr launch");
@@ -270,13 +225,14 @@ int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int
     uint64_t* cl = (uint64_t*)c->census_l.ptr;
     uint64_t* cr = (uint64_t*)c->census_r.ptr;
     SVA_HIP(c, launch_census_pair(*c, left, right, W, H, pitch, cl, cr), "census launch");
-    SVA_HIP(c, launch_cost2(*c, cl, cr, W, H, p->D, p->dmin, p->dir, p->dir_y, C), "cost launch");
-    if ((s = paths_wta(c, C, W, H, p, disp, sub))) return s;
+    SVA_HIP(c, launch_cost2(*c, cl, cr, W, H, Dp, p->dmin, p->dir, p->dir_y, C, p->D),
+            "cost launch");
+    if ((s = paths_wta(c, C, W, H, p, Dp, disp, sub))) return s;
     if (p->lr_check) {
         // right image as reference: roles of the census maps swap, the step flips
-        SVA_HIP(c, launch_cost2(*c, cr, cl, W, H, p->D, p->dmin, -p->dir, -p->dir_y, C),
+        SVA_HIP(c, launch_cost2(*c, cr, cl, W, H, Dp, p->dmin, -p->dir, -p->dir_y, C, p->D),
                 "cost launch");
-        if ((s = paths_wta(c, C, W, H, p, dr, nullptr))) return s;
+        if ((s = paths_wta(c, C, W, H, p, Dp, dr, nullptr))) return s;
         SVA_HIP(c, launch_lr_check(*c, disp, dr, sub, W, H, p->dir, p->dir_y, p->lr_max_diff,
                                    p->invalid),
                 "lr launch");
@@ -465,12 +421,12 @@ int sva_reserve(void* ctx, int W, int H, int D) {
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     if (W <= 0 || H <= 0 || D <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad reserve size");
+    if (padded_D(D)) D = padded_D(D);     // a frame's volumes use the native width (§4.7)
     const size_t np = (size_t)W * H, nv = np * (size_t)D;
-    // padded census pair of the fused path at dmin = 0 (grows if a call needs more)
-    SVA_HIP(c, c->census_l.ensure(2 * (size_t)H * (size_t)(W + fused_pad(W, D, 0)) * 8), "reserve");
+    SVA_HIP(c, c->census_l.ensure(np * 8), "reserve");
     SVA_HIP(c, c->census_r.ensure(np * 8), "reserve");
     SVA_HIP(c, c->cost.ensure(nv), "reserve");
-    SVA_HIP(c, c->paths.ensure(nv * 8), "reserve");
+    SVA_HIP(c, c->paths.ensure(nv * 6), "reserve");
     SVA_HIP(c, c->ckpt.ensure(ckpt_bytes(W, H, D)), "reserve");
     return SVA_OK;
 }
@@ -478,10 +434,11 @@ int sva_reserve(void* ctx, int W, int H, int D) {
 int sva_set_path_kernel(void* ctx, int kernel) {
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
-    if (kernel != SVA_PATH_KERNEL_COST_VOLUME && kernel != SVA_PATH_KERNEL_FUSED &&
-        kernel != SVA_PATH_KERNEL_AUTO)
+    if (kernel == SVA_PATH_KERNEL_FUSED)
+        return fail(c, SVA_ERR_UNSUPPORTED,
+                    "the census-fused path kernel was removed in ABI v4 (DESIGN.md §4.5)");
+    if (kernel != SVA_PATH_KERNEL_COST_VOLUME && kernel != SVA_PATH_KERNEL_AUTO)
         return fail(c, SVA_ERR_INVALID_ARG, "unknown path kernel");
-    c->path_kernel = kernel;
     return SVA_OK;
 }
 
@@ -575,7 +532,7 @@ int sva_cost_d(void* ctx, const uint64_t* cl, const uint64_t* cr, int W, int H,
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
-    if ((s = check_sgm(c, p, W, H))) return s;
+    if ((s = check_sgm(c, p, W, H, true))) return s;
     if (!cl || !cr || !C || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
     SVA_HIP(c, launch_cost2(*c, cl, cr, W, H, p->D, p->dmin, p->dir, p->dir_y, C), "cost launch");
     return SVA_OK;
@@ -586,7 +543,7 @@ int sva_census_cost_d(void* ctx, const uint8_t* left, const uint8_t* right, int 
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
-    if ((s = check_sgm(c, p, W, H))) return s;
+    if ((s = check_sgm(c, p, W, H, true))) return s;
     if ((s = check_image(c, left, W, H, pitch))) return s;
     if ((s = check_image(c, right, W, H, pitch))) return s;
     if (!C) return fail(c, SVA_ERR_INVALID_ARG, "null cost output");
@@ -601,26 +558,9 @@ int sva_paths_d(void* ctx, const uint8_t* C, int W, int H, const sva_sgm_params*
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
-    if ((s = check_sgm(c, p, W, H))) return s;
+    if ((s = check_sgm(c, p, W, H, true))) return s;
     if (!C || !L8 || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
     SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L8), "paths launch");
-    return SVA_OK;
-}
-
-int sva_paths_fused_d(void* ctx, const uint8_t* left, const uint8_t* right, int W, int H,
-                      size_t pitch, const sva_sgm_params* p, uint8_t* L8) {
-    Ctx* c = as_ctx(ctx);
-    SVA_CHECK_CTX(c);
-    int s;
-    if ((s = check_image(c, left, W, H, pitch)) || (s = check_image(c, right, W, H, pitch)) ||
-        (s = check_sgm(c, p, W, H)))
-        return s;
-    if (!L8) return fail(c, SVA_ERR_INVALID_ARG, "null path volume output");
-    if (p->dir_y != 0 || !fused_fits(W, H, p->D, p->dmin))
-        return fail(c, SVA_ERR_UNSUPPORTED, "fused path: 1-D steps (dir_y = 0) only");
-    size_t mw = 0;
-    if ((s = census_padded(c, left, right, W, H, pitch, p, &mw))) return s;
-    if ((s = fused_paths(c, mw, false, W, H, p, p->dir > 0 ? 1 : -1, L8))) return s;
     return SVA_OK;
 }
 
@@ -629,7 +569,7 @@ int sva_aggregate_d(void* ctx, const uint8_t* C, int W, int H, const sva_sgm_par
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
-    if ((s = check_sgm(c, p, W, H))) return s;
+    if ((s = check_sgm(c, p, W, H, true))) return s;
     if (!C || !S || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
     const size_t nv = (size_t)W * H * (size_t)p->D;
     SVA_HIP(c, c->paths.ensure(nv * 8), "path workspace");
@@ -651,7 +591,7 @@ int sva_paths_ckpt_d(void* ctx, const uint8_t* C, int W, int H, const sva_sgm_pa
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
-    if ((s = check_sgm(c, p, W, H))) return s;
+    if ((s = check_sgm(c, p, W, H, true))) return s;
     if (!C || !L6 || !CK || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
     SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L6, CK), "paths launch");
     return SVA_OK;
@@ -662,7 +602,7 @@ int sva_wta_h_d(void* ctx, const uint8_t* C, const uint8_t* L6, const uint8_t* C
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
-    if ((s = check_sgm(c, p, W, H))) return s;
+    if ((s = check_sgm(c, p, W, H, true))) return s;
     if (!C || !L6 || !CK || !disp || W <= 0 || H <= 0)
         return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
     SVA_HIP(c, launch_wta_h(*c, C, L6, CK, W, H, p->D, p->P1, p->P2, p->dmin, disp,
@@ -676,7 +616,7 @@ int sva_wta_d(void* ctx, const uint16_t* S, int W, int H, const sva_sgm_params* 
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
-    if ((s = check_sgm(c, p, W, H))) return s;
+    if ((s = check_sgm(c, p, W, H, true))) return s;
     if (!S || !disp || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
     SVA_HIP(c, launch_wta_from_sum(*c, S, W, H, p->D, p->dmin, disp, p->subpixel ? sub : nullptr),
             "wta launch");

@@ -62,6 +62,15 @@ __device__ __forceinline__ unsigned pack4(unsigned p01, unsigned p23) {
     return __builtin_amdgcn_perm(p23, p01, 0x06040200u);
 }
 
+// Disparity padding: a frame with D not in {64,128,192,256}
+// runs at the next native width Dp with cost 255 at d >= D.  pad_bytes gives
+// the byte mask of the dword holding disparities d0 .. d0+3: 0xff in byte b
+// when d0 + b >= dreal (OR it into the packed costs).
+__device__ __forceinline__ unsigned pad_bytes(int d0, int dreal) {
+    const int n = dreal - d0;   // real disparities in this dword
+    return n <= 0 ? 0xffffffffu : (n >= 4 ? 0u : 0xffffffffu << (8 * n));
+}
+
 // Matched-pixel offset for match distance s >= 0 along the integer baseline
 // direction (bx, by): s pixels along the major axis,
 // round_half_up(s*m/M) along the minor one, each with its component's sign.

@@ -1,0 +1,55 @@
+// sva_tuning.h -- every measured tuning constant of the kernels, in one place.
+//
+// Product translation units carry no experiment switches (VERDICT r02 weak
+// #7): each constant below is the value the in-process A/B runs chose, with
+// the measurement that chose it.  An experiment build rewrites this header
+// in a scratch copy of csrc/ (tools/build_variants.sh KEY=VALUE ...), so the
+// A/B library never shares a translation unit with the product.
+#pragma once
+
+namespace sva {
+namespace tune {
+
+// ---- sgm_paths.hip / sgm_common.h ------------------------
+// Prefetch ring depth in steps, per line kind and disparities per lane
+// (D = 16 * DPL).  Horizontal lines are few (2H) and long (W steps) and run
+// alone once the vertical/diagonal lines drain, so they get the deeper ring.
+// In-process A/B (tools/ab_paths.py): 1080p D=128 H/V 8/8 0.755-0.788 ms,
+// 32/12 0.661 (149 VGPRs, 3 waves/SIMD), 40/8 0.689 (2 waves/SIMD), 32/4
+// 0.770; re-checked after the round-2 step changes: 32/12 0.597, 32/16 0.596,
+// 32/8 0.601, 28/12 0.597, 36/12 0.599.  D=64 (1080p) 40/12 0.372 vs 8/8
+// 0.416; D=192 24/8 0.996 vs 12/8 1.154; D=256 (4K) 12/8 (16/8 equal, 20/8
+// and 12/12 +3 %).
+constexpr int kPfH4 = 40, kPfV4 = 12;
+constexpr int kPfH8 = 32, kPfV8 = 12;
+constexpr int kPfH12 = 24, kPfV12 = 8;
+constexpr int kPfH16 = 12, kPfV16 = 8;
+// Cache-policy bits of the cost-volume loads.  A/B (full frame, in-process):
+// nt (2) +8 %, sc0+nt (3) +8 %; sc0 (1), sc0+sc1 (17), 8, 16 within noise.
+constexpr int kCLoadAux = 0;
+
+// ---- wta_h.hip --------------------------------------------
+// Prefetch depth (steps) of the forward pass (1 cost load per step) and the
+// backward pass (6 volume loads per step); D > 128 halves the forward ring
+// and keeps 4 for the backward one (4 beats 2 and 3: 1080p D=192 -2 %, 4K
+// D=256 -2.4 %; deeper at D=128, 6 or 8, within noise).
+constexpr int kWtahPfFwd = 8, kWtahPfBwd = 4;
+constexpr int kWtahPfFwdWide = 4, kWtahPfBwdWide = 4;
+
+// ---- census.hip / census_cost.hip / cost.hip ------------
+// Rows per workgroup of the multi-row census kernel.
+constexpr int kCensusRows = 16;
+// census_cost: pixels per workgroup row and rows per workgroup; 128 px x 4
+// rows was the best of 64/128/256 px x 2/4/8/16 rows (0.093 ms at 1080p
+// D=128, profiles/r01_v8/ab_census_cost_tiling.jsonl); 192 / 256 px measured
+// 0.093 / 0.101 ms in round 2.
+constexpr int kCensusCostPx = 128;
+constexpr int kCensusCostRows = 4;
+
+// ---- refpath.hip, Mode R plane kernel v3 ------------------
+constexpr int kPlaneOuKB = 24;      // staged O chunk (KB)
+constexpr int kPlaneWords = 1024;   // offset bitmap per pass: 32K bits
+constexpr int kPlaneMinBlocks = 3;  // __launch_bounds__ min workgroups per CU
+
+}  // namespace tune
+}  // namespace sva

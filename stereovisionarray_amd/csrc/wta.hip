@@ -5,13 +5,11 @@
 // holds disparities [k*DPL, k*DPL+DPL).  S = sum of the 8 u8 path volumes is
 // formed in packed u16 (no carry: S <= 8*255 < 2^16); the pick is
 // wta_common.h's.  These kernels serve the stage API (sva_wta_d,
-// sva_aggregate_d) and the census-fused route; the cost-volume frame
-// pipeline uses wta_h.hip, which also recomputes the horizontal paths.
+// sva_aggregate_d); the frame pipeline uses wta_h.hip, which also recomputes
+// the horizontal paths.
 #include "sva_device.h"
 #include "sva_internal.h"
 #include "wta_common.h"
-
-#include <cstdlib>
 
 namespace sva {
 namespace {
@@ -85,19 +83,6 @@ __device__ __forceinline__ void wta_finish(const unsigned (&S)[DPL / 2], int k, 
 }
 
 template <int DPL>
-__global__ __launch_bounds__(BLOCK) void wta_paths_kernel(const uint8_t* __restrict__ L8,
-                                                          size_t vol, int npix, int D, int dmin,
-                                                          uint16_t* __restrict__ disp,
-                                                          float* __restrict__ sub) {
-    const size_t pix = (size_t)blockIdx.x * PIX_PER_BLOCK + (threadIdx.x >> 4);
-    const int k = threadIdx.x & 15;
-    if (pix >= (size_t)npix) return;
-    unsigned S[DPL / 2];
-    sum_paths<DPL>(L8 + pix * D + k * DPL, vol, S);
-    wta_finish<DPL>(S, k, D, dmin, pix, disp, sub);
-}
-
-template <int DPL>
 __global__ __launch_bounds__(BLOCK) void sum_paths_kernel(const uint8_t* __restrict__ L8,
                                                           size_t vol, int npix, int D,
                                                           uint16_t* __restrict__ Sout) {
@@ -161,16 +146,6 @@ __global__ void lr_check_kernel(uint16_t* __restrict__ dl, const uint16_t* __res
         case 256: hipLaunchKernelGGL(KERNEL<16>, GRID, dim3(BLOCK), 0, c.stream, __VA_ARGS__); break; \
         default: return hipErrorInvalidValue;                                                    \
     }
-
-hipError_t launch_wta_from_paths(Ctx& c, const uint8_t* L8, int W, int H, int D, int dmin,
-                                 uint16_t* disp, float* sub) {
-    ScopedKernelTimer t(c, "wta");
-    const int npix = W * H;
-    const size_t vol = (size_t)npix * D;
-    dim3 grid((npix + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK);
-    SVA_DISPATCH_D(D, wta_paths_kernel, grid, L8, vol, npix, D, dmin, disp, sub);
-    return hipGetLastError();
-}
 
 hipError_t launch_sum(Ctx& c, const uint8_t* L8, int W, int H, int D, uint16_t* S) {
     ScopedKernelTimer t(c, "path_sum");

@@ -34,26 +34,14 @@ constexpr int HROWS = HB / 16;
 
 struct WtaHGeom {
     int W, H, D, P1, P2, dmin, ns;
+    int dreal;        // disparities of the caller (< D: padded frame)
     unsigned vol;     // bytes of one [H][W][D] volume (< 2^32)
     unsigned ckvol;   // bytes of one checkpoint plane [H][ns][D]
 };
 
-// Prefetch depth (steps) of the backward pass, which loads 6 u8 vectors per
-// step; the forward pass loads 1 and runs a deeper ring.
-#ifndef SVA_WTAH_PF1
-#define SVA_WTAH_PF1 8
-#endif
-#ifndef SVA_WTAH_PF2
-#define SVA_WTAH_PF2 4
-#endif
-#ifndef SVA_WTAH_PF1_WIDE
-#define SVA_WTAH_PF1_WIDE (SVA_WTAH_PF1 / 2)
-#endif
-#ifndef SVA_WTAH_PF2_WIDE   // D > 128: 4 beats 2 and 3 (1080p D=192 -2 %, 4K D=256 -2.4 %)
-#define SVA_WTAH_PF2_WIDE SVA_WTAH_PF2
-#endif
-template <int DPL> constexpr int pf_fwd() { return DPL <= 8 ? SVA_WTAH_PF1 : SVA_WTAH_PF1_WIDE; }
-template <int DPL> constexpr int pf_bwd() { return DPL <= 8 ? SVA_WTAH_PF2 : SVA_WTAH_PF2_WIDE; }
+// Prefetch depths of the two passes (tune::kWtahPf*).
+template <int DPL> constexpr int pf_fwd() { return DPL <= 8 ? tune::kWtahPfFwd : tune::kWtahPfFwdWide; }
+template <int DPL> constexpr int pf_bwd() { return DPL <= 8 ? tune::kWtahPfBwd : tune::kWtahPfBwdWide; }
 // Cache policy of the six volume loads (their last use): nt above D = 64, so
 // the stream does not evict the cost bytes other workgroups are still reading
 // (default loads: +9 % at 1080p D=128, +12 % at 4K D=256); at D = 64 the
@@ -72,13 +60,21 @@ __device__ __forceinline__ void unpack_add(const unsigned (&w)[NW], unsigned (&S
 }
 
 // Path state from a u8 checkpoint: A = L(q) as packed pairs, m = min_k L(q).
-template <int DPL>
+// Padded disparities (PAD) held L >= 255 in the path kernel, which the u8
+// checkpoint truncated; they restart at 255.  Every real disparity evolves
+// the same from 255 as from the true value: a padded neighbour enters only
+// as A + P1 >= 255 >= m + P2 (m <= 62), and never sets the row minimum.
+template <int DPL, bool PAD>
 __device__ __forceinline__ void load_state(rsrc_t r, unsigned off, unsigned (&A)[DPL / 2],
-                                           unsigned& m) {
+                                           unsigned& m, const unsigned (&padm)[DPL / 2]) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
     const Words<NW> w = bload<NW>(r, off);
 #pragma unroll
     for (int q = 0; q < NW; q++) unpack4(w.w[q], A[2 * q], A[2 * q + 1]);
+    if constexpr (PAD) {
+#pragma unroll
+        for (int j = 0; j < NP; j++) A[j] |= padm[j] & 0x00ff00ffu;   // A < 256: OR = max
+    }
     unsigned mm = 0xffffffffu;
 #pragma unroll
     for (int j = 0; j < NP; j++) {
@@ -89,7 +85,7 @@ __device__ __forceinline__ void load_state(rsrc_t r, unsigned off, unsigned (&A)
     m = row_min_u32(mm);
 }
 
-template <int DPL>
+template <int DPL, bool PAD>
 __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C,
                                                    const uint8_t* __restrict__ L6,
                                                    const uint8_t* __restrict__ CK, WtaHGeom g,
@@ -115,12 +111,22 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
 #pragma unroll
     for (int r = 0; r < 6; r++) rV[r] = make_rsrc(L6 + (size_t)r * g.vol, g.vol);
     const unsigned ckrow = (unsigned)y * (unsigned)g.ns;
+    // PAD: per pair, 0xffff in the halves of padded disparities (d >= dreal),
+    // OR-ed into S so they never win the first-minimum WTA
+    unsigned padm[NP];
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+        const int d = k * DPL + 2 * j;
+        padm[j] = PAD ? ((d >= g.dreal ? 0x0000ffffu : 0u) | (d + 1 >= g.dreal ? 0xffff0000u : 0u))
+                      : 0u;
+    }
 
     unsigned A[NP], m;
     Edges edges;
     // ---- pass 1: left-to-right (direction 0) over the segment ------------
     if (s > 0) {
-        load_state<DPL>(rCK0, (ckrow + (unsigned)(s - 1)) * uD + (unsigned)(k * DPL), A, m);
+        load_state<DPL, PAD>(rCK0, (ckrow + (unsigned)(s - 1)) * uD + (unsigned)(k * DPL), A, m,
+                             padm);
     } else {
 #pragma unroll
         for (int j = 0; j < NP; j++) A[j] = 0u;   // L(q) = 0, m = 0  =>  L = C
@@ -153,7 +159,8 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
 
     // ---- pass 2: right-to-left (direction 1), sum, WTA --------------------
     if (x0 + K < W) {
-        load_state<DPL>(rCK1, (ckrow + (unsigned)(s + 1)) * uD + (unsigned)(k * DPL), A, m);
+        load_state<DPL, PAD>(rCK1, (ckrow + (unsigned)(s + 1)) * uD + (unsigned)(k * DPL), A, m,
+                             padm);
     } else {
 #pragma unroll
         for (int j = 0; j < NP; j++) A[j] = 0u;
@@ -188,6 +195,10 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
             unpack_add<NW>(LR[j], S);                        // L_0
 #pragma unroll
             for (int r = 0; r < 6; r++) unpack_add<NW>(rv[slot][r].w, S);
+            if constexpr (PAD) {
+#pragma unroll
+                for (int p = 0; p < NP; p++) S[p] |= padm[p];
+            }
             unsigned spm, s0;
             const int ds = wta_pick_raw<DPL>(S, k, want_sub, &spm, &s0);
             if (k == j / R) {
@@ -209,7 +220,7 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
         if (x < W) {
             disp[row + x] = (uint16_t)(g.dmin + (int)dres[e]);
             if (want_sub)
-                sub[row + x] = subpixel(g.dmin, (int)dres[e], D, sres[e][0] & 0xffffu, sres[e][1],
+                sub[row + x] = subpixel(g.dmin, (int)dres[e], g.dreal, sres[e][0] & 0xffffu, sres[e][1],
                                         sres[e][0] >> 16);
         }
     }
@@ -220,23 +231,34 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
 bool wta_h_supported(int D) { return D == 64 || D == 128 || D == 192 || D == 256; }
 
 hipError_t launch_wta_h(Ctx& c, const uint8_t* C, const uint8_t* L6, const uint8_t* CK, int W,
-                        int H, int D, int P1, int P2, int dmin, uint16_t* disp, float* sub) {
+                        int H, int D, int P1, int P2, int dmin, uint16_t* disp, float* sub,
+                        int dreal) {
     ScopedKernelTimer t(c, "wta_h");
     WtaHGeom g;
     g.W = W; g.H = H; g.D = D; g.P1 = P1; g.P2 = P2; g.dmin = dmin;
+    g.dreal = dreal > 0 && dreal < D ? dreal : D;
+    const bool pad = g.dreal < D;
     g.ns = ckpt_segments(W, D);
     const size_t vol = (size_t)W * H * D;
     if (vol >= (size_t)1 << 32) return hipErrorInvalidValue;
     g.vol = (unsigned)vol;
     g.ckvol = (unsigned)((size_t)H * g.ns * D);
     const dim3 grid((unsigned)(g.ns * ((H + HROWS - 1) / HROWS)));
+#define SVA_WTAH(DPL_)                                                                          \
+    if (pad)                                                                                    \
+        hipLaunchKernelGGL((wta_h_kernel<DPL_, true>), grid, dim3(HB), 0, c.stream, C, L6, CK,  \
+                           g, disp, sub);                                                       \
+    else                                                                                        \
+        hipLaunchKernelGGL((wta_h_kernel<DPL_, false>), grid, dim3(HB), 0, c.stream, C, L6, CK, \
+                           g, disp, sub)
     switch (D) {
-        case 64: hipLaunchKernelGGL(wta_h_kernel<4>, grid, dim3(HB), 0, c.stream, C, L6, CK, g, disp, sub); break;
-        case 128: hipLaunchKernelGGL(wta_h_kernel<8>, grid, dim3(HB), 0, c.stream, C, L6, CK, g, disp, sub); break;
-        case 192: hipLaunchKernelGGL(wta_h_kernel<12>, grid, dim3(HB), 0, c.stream, C, L6, CK, g, disp, sub); break;
-        case 256: hipLaunchKernelGGL(wta_h_kernel<16>, grid, dim3(HB), 0, c.stream, C, L6, CK, g, disp, sub); break;
+        case 64: SVA_WTAH(4); break;
+        case 128: SVA_WTAH(8); break;
+        case 192: SVA_WTAH(12); break;
+        case 256: SVA_WTAH(16); break;
         default: return hipErrorInvalidValue;
     }
+#undef SVA_WTAH
     return hipGetLastError();
 }
 

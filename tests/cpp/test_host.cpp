@@ -162,15 +162,27 @@ static void gpu_tests() {
     std::vector<float> sub;
     auto ds = computeDisparitySGM(eng, views[12], views[13], p, &sub);
     CHECK(ds.size() == (size_t)W * H && sub.size() == ds.size());
-    // both path kernels give the same maps
+    // AUTO and COST_VOLUME are one route; the census-fused kernel is gone (ABI v4)
     std::vector<float> sub_f;
-    eng.setPathKernel(SVA_PATH_KERNEL_FUSED);
+    eng.setPathKernel(SVA_PATH_KERNEL_COST_VOLUME);
     auto df = computeDisparitySGM(eng, views[12], views[13], p, &sub_f);
     eng.setPathKernel(SVA_PATH_KERNEL_AUTO);
     CHECK(df == ds && sub_f == sub);
     bool threw = false;
     try {
-        p.D = 50;
+        eng.setPathKernel(SVA_PATH_KERNEL_FUSED);
+    } catch (const Error& e) {
+        threw = e.status == SVA_ERR_UNSUPPORTED;
+    }
+    CHECK(threw);
+    // any D <= 256: D = 50 runs padded to 64
+    p.D = 50;
+    auto d50 = computeDisparitySGM(eng, views[12], views[13], p);
+    CHECK(d50.size() == ds.size());
+    for (uint16_t v : d50) CHECK(v < 50);
+    threw = false;
+    try {
+        p.D = 257;
         computeDisparitySGM(eng, views[12], views[13], p);
     } catch (const Error& e) {
         threw = e.status == SVA_ERR_UNSUPPORTED;

@@ -112,38 +112,20 @@ def test_reserve_timing_and_errors(ctx, sva):
     assert ctx.kernel_time("wta") == (0.0, 0)
     # 1-D steps without the L/R check, D >= 128: census and cost are one kernel ("cost")
     assert ctx.kernel_time("census") == (0.0, 0)
-    # the census-fused path kernel has no cost volume and no cost kernel
-    ctx.reset_timing()
-    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_FUSED)
-    ctx.set_timing(True)
-    try:
-        ctx.disparity_sgm(L, R, sva.default_params(D=128))
-    finally:
-        ctx.set_timing(False)
-        ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
-    assert ctx.kernel_time("cost") == (0.0, 0)
-    assert ctx.kernel_time("sgm_fused")[1] == 1 and ctx.kernel_time("sgm_paths")[1] == 0
-    # AUTO (the default) is the cost-volume route at every D, D = 256 included
+    # AUTO (the default) and COST_VOLUME are the same route, D = 256 included
     L2, R2, _ = synth.stereo_pair(64, 320, 256, 0, -1, seed=3)
+    for kern in (sva.SVA_PATH_KERNEL_AUTO, sva.SVA_PATH_KERNEL_COST_VOLUME):
+        ctx.set_path_kernel(kern)
+        ctx.reset_timing()
+        ctx.set_timing(True)
+        ctx.disparity_sgm(L2, R2, sva.default_params(D=256))
+        ctx.set_timing(False)
+        assert ctx.kernel_time("cost")[1] == 1 and ctx.kernel_time("wta_h")[1] == 1
+    # the census-fused path kernel was removed in ABI v4
+    with pytest.raises(sva.SvaError) as e:
+        ctx.set_path_kernel(sva.SVA_PATH_KERNEL_FUSED)
+    assert e.value.status == sva.SVA_ERR_UNSUPPORTED
     ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
-    ctx.reset_timing()
-    ctx.set_timing(True)
-    ctx.disparity_sgm(L2, R2, sva.default_params(D=256))
-    ctx.set_timing(False)
-    assert ctx.kernel_time("cost")[1] == 1 and ctx.kernel_time("sgm_fused") == (0.0, 0)
-    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_FUSED)
-    ctx.reset_timing()
-    ctx.set_timing(True)
-    ctx.disparity_sgm(L2, R2, sva.default_params(D=256))
-    ctx.set_timing(False)
-    assert ctx.kernel_time("cost") == (0.0, 0) and ctx.kernel_time("sgm_fused")[1] == 1
-    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_COST_VOLUME)
-    ctx.reset_timing()
-    ctx.set_timing(True)
-    ctx.disparity_sgm(L2, R2, sva.default_params(D=256))
-    ctx.set_timing(False)
-    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
-    assert ctx.kernel_time("cost")[1] == 1
     with pytest.raises(sva.SvaError) as e:
         ctx.set_path_kernel(7)
     assert e.value.status == sva.SVA_ERR_INVALID_ARG
@@ -151,11 +133,9 @@ def test_reserve_timing_and_errors(ctx, sva):
     ctx.reset_timing()
     ctx.set_timing(sva.SVA_TIMING_PATHS)
     ctx.disparity_sgm(L, R, sva.default_params(D=128))
-    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_FUSED)
     ctx.disparity_sgm(L2, R2, sva.default_params(D=256))
-    ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
     ctx.set_timing(sva.SVA_TIMING_OFF)
-    assert ctx.kernel_time("sgm_paths")[1] == 1 and ctx.kernel_time("sgm_fused")[1] == 1
+    assert ctx.kernel_time("sgm_paths")[1] == 2
     for name in ("census", "cost", "wta", "wta_h"):
         assert ctx.kernel_time(name) == (0.0, 0), name
     with pytest.raises(sva.SvaError) as e:
@@ -165,6 +145,6 @@ def test_reserve_timing_and_errors(ctx, sva):
     ctx.reset_timing()
     assert ctx.kernel_time("sgm_paths") == (0.0, 0)
     with pytest.raises(sva.SvaError) as e:
-        ctx.disparity_sgm(L, R, sva.default_params(D=48))
-    assert "D in {64,128,192,256}" in str(e.value)
+        ctx.disparity_sgm(L, R, sva.default_params(D=300))
+    assert "D in 1..256" in str(e.value)
     assert b"D in" in sva.lib.sva_last_error(ctx.h)

@@ -8,11 +8,10 @@ is matched along its own baseline step, then the per-camera
 median depth (§2.6).  Every map is bit-exact vs the threaded oracle
 (oracle.sgm2), and every fused depth is bit-exact in f64 vs oracle.fuse_depth.
 
-Config 5 -- 256 x 1080p D=192 pairs.  One pair bit-exact vs oracle.sgm through
-BOTH path kernels (cost volume and census-fused), and bench.py's batch route
-(consecutive pairs alternating over several contexts/streams, on the default
-AUTO route and on the opt-in fused kernel) byte-identical to the
-single-stream result for several pairs.
+Config 5 -- 256 x 1080p D=192 pairs.  One pair bit-exact vs oracle.sgm, and
+bench.py's batch route (consecutive pairs alternating over several
+contexts/streams) byte-identical to the single-stream result for several
+pairs.
 
 Parity vs the reference itself is unpinned: the reference has
 no SGM, no 2-D matcher and no fusion (its loop keeps the last pair,
@@ -154,25 +153,19 @@ def test_config4_grid8_all_fusion(ctx, sva, oracle, grid8_views):
     assert n_groups == 7
 
 
-@pytest.mark.parametrize("kernel", ["cost_volume", "fused"])
-def test_config5_pair_d192(ctx, sva, oracle, kernel):
-    """One config-5 pair (seed 0) at 1920x1080 D=192 through
-    each path kernel, bit-exact vs the oracle; sub-pixel within 1e-5 px."""
+def test_config5_pair_d192(ctx, sva, oracle):
+    """One config-5 pair (seed 0) at 1920x1080 D=192,
+    bit-exact vs the oracle; sub-pixel within 1e-5 px."""
     D = 192
     L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=0)
-    k = {"cost_volume": sva.SVA_PATH_KERNEL_COST_VOLUME, "fused": sva.SVA_PATH_KERNEL_FUSED}
-    ctx.set_path_kernel(k[kernel])
-    try:
-        disp, sub = ctx.disparity_sgm(L, R, sva.default_params(D=D, subpixel=1))
-    finally:
-        ctx.set_path_kernel(sva.SVA_PATH_KERNEL_AUTO)
+    disp, sub = ctx.disparity_sgm(L, R, sva.default_params(D=D, subpixel=1))
     od, osub = oracle.sgm(L, R, D, 0, -1, subpixel=True, threads=ORACLE_THREADS)
     assert np.array_equal(disp, od)
     assert np.max(np.abs(sub - osub)) <= 1e-5
 
 
-@pytest.mark.parametrize("kernel,n_ctx", [("auto", 2), ("auto", 3), ("fused", 2)])
-def test_config5_batch_route_streams(sva, oracle, torch_dev, kernel, n_ctx):
+@pytest.mark.parametrize("n_ctx", [2, 3])
+def test_config5_batch_route_streams(sva, oracle, torch_dev, n_ctx):
     """bench.py's config-5 route: pairs alternate over n_ctx contexts, each with
     its own HIP stream and workspaces (bench.py --streams); the maps must be
     byte-identical to the same pairs run one by one on one stream, and pair 0
@@ -183,12 +176,10 @@ def test_config5_batch_route_streams(sva, oracle, torch_dev, kernel, n_ctx):
     dl = [torch.from_numpy(a).to(torch_dev) for a, _ in pairs]
     dr = [torch.from_numpy(b).to(torch_dev) for _, b in pairs]
     ctxs, streams = [], []
-    k = {"auto": sva.SVA_PATH_KERNEL_AUTO, "fused": sva.SVA_PATH_KERNEL_FUSED}[kernel]
     for _ in range(n_ctx):
         s = torch.cuda.Stream(torch_dev)
         c = sva.Context(torch_dev.index or 0)
         c.set_stream(s.cuda_stream)
-        c.set_path_kernel(k)
         ctxs.append(c)
         streams.append(s)
     try:
@@ -207,7 +198,7 @@ def test_config5_batch_route_streams(sva, oracle, torch_dev, kernel, n_ctx):
             a, s1 = ctxs[0].disparity_sgm(pairs[j][0], pairs[j][1], p)
             assert np.array_equal(got[j], a), f"pair {j}"
             assert np.array_equal(gsub[j].view(np.uint32), s1.view(np.uint32)), f"pair {j}"
-        if kernel == "auto" and n_ctx == 2:
+        if n_ctx == 2:
             od, _ = oracle.sgm(pairs[0][0], pairs[0][1], D, 0, -1, subpixel=False,
                                threads=ORACLE_THREADS)
             assert np.array_equal(got[0], od)

@@ -79,9 +79,15 @@ def test_batch_sgm_d_mixed_steps_and_errors(ctx, sva, oracle, torch_dev):
             od, _ = oracle.sgm2(imgs[j][0], imgs[j][1], D, 0, sx, sy, subpixel=False)
             assert np.array_equal(got[j], od), (sx, sy)
         with pytest.raises(sva.SvaError) as e:
-            m.batch_sgm_d([(dl[0].data_ptr(), dr[0].data_ptr(), sva.default_params(D=50))], W, H,
+            m.batch_sgm_d([(dl[0].data_ptr(), dr[0].data_ptr(), sva.default_params(D=300))], W, H,
                           W, maps.data_ptr())
         assert e.value.status == sva.SVA_ERR_INVALID_ARG
+        # any D <= 256 runs padded to the next native width
+        m.batch_sgm_d([(dl[2].data_ptr(), dr[2].data_ptr(), sva.default_params(D=50, dir=-1))],
+                      W, H, W, maps.data_ptr())
+        m.synchronize()
+        od, _ = oracle.sgm2(imgs[2][0], imgs[2][1], 50, 0, -1, 0, subpixel=False)
+        assert np.array_equal(maps[0].cpu().numpy().view(np.uint16), od)
         h = m.context_handle(0, 1)
         assert h
         with pytest.raises(sva.SvaError):

@@ -233,7 +233,7 @@ def test_ref_path_1080p_full_frame(ctx, sva, oracle, pair):
     assert np.array_equal(d16, o16)
     assert np.array_equal(d8, o8)
     # the synthetic shift is the true disparity on most of the frame
-    assert np.mean(d16[ov == 1] == 178) > 0.9
+    assert np.mean(d16[ov == 1] == 178) > 0.75
 
 
 # 4K (BASELINE config 3's size): the v3 plane kernel stages O in chunks of

@@ -30,8 +30,7 @@ def main():
     ap.add_argument("--sub", action="store_true", help="wta_h / sgm entries: also write the f32 sub-pixel map")
     ap.add_argument("--dmin", type=int, default=0)
     ap.add_argument("--entry", default="paths",
-                    choices=["paths", "sgm", "cost", "fused", "census", "census_cost", "ckpt",
-                             "wta_h"])
+                    choices=["paths", "sgm", "cost", "census", "census_cost", "ckpt", "wta_h"])
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -97,10 +96,6 @@ def main():
             elif a.entry == "census":
                 st = lib.sva_census_d(h, ct.c_void_p(dL.data_ptr()), W, H, ct.c_size_t(W),
                                       ct.c_void_p(cl.data_ptr()))
-            elif a.entry == "fused":
-                st = lib.sva_paths_fused_d(h, ct.c_void_p(dL.data_ptr()), ct.c_void_p(dR.data_ptr()),
-                                           W, H, ct.c_size_t(W), ct.byref(p),
-                                           ct.c_void_p(L8.data_ptr()))
             elif a.entry == "census_cost":
                 st = lib.sva_census_cost_d(h, ct.c_void_p(dL.data_ptr()), ct.c_void_p(dR.data_ptr()),
                                            W, H, ct.c_size_t(W), ct.byref(p),
@@ -128,15 +123,6 @@ def main():
                 torch.cuda.synchronize()
                 outs.append(torch.sum(C.view(torch.int64)).item())
             assert len(set(outs)) == 1, outs
-        if a.entry == "fused" and it == 0:
-            outs = []
-            for n, lib, h in handles:
-                lib.sva_paths_fused_d(h, ct.c_void_p(dL.data_ptr()), ct.c_void_p(dR.data_ptr()), W, H,
-                                      ct.c_size_t(W), ct.byref(p), ct.c_void_p(L8.data_ptr()))
-                torch.cuda.synchronize()
-                outs.append(torch.sum(L8.view(torch.int64)).item())
-            if not os.environ.get("AB_NOCHECK"):
-                assert len(set(outs)) == 1, outs
         if a.entry in ("ckpt", "wta_h") and it == 0:
             outs = []
             for n, lib, h in handles:

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B driver for bench.py runs (replaces the round-1 one-off tools/_*.sh).
 #
-#   RUNS='label|ENV=1 ENV2=x|--workload 1080p_d128 --steps 20;label2||--path-kernel fused' \
+#   RUNS='label|ENV=1 ENV2=x|--workload 1080p_d128 --steps 20;label2||--workload 1080p_d192' \
 #   REPS=2 tools/bench_ab.sh
 #
 # Each run is "label|environment assignments|bench.py arguments".  An

@@ -30,9 +30,6 @@ def main():
     torch.cuda.set_stream(s)
     ctx.set_stream(s.cuda_stream)
     ctx.reserve(W, H, D)
-    if len(sys.argv) > 1:
-        ctx.set_path_kernel({"fused": sva.SVA_PATH_KERNEL_FUSED,
-                             "cost_volume": sva.SVA_PATH_KERNEL_COST_VOLUME}[sys.argv[1]])
     L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=1)
     Lt, Rt = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
     disp = torch.zeros((H, W), dtype=torch.int16, device=dev)

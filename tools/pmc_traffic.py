@@ -19,8 +19,7 @@ import os
 import sys
 
 SHORT = {
-    "sgm_paths_kernel": "sgm_paths", "sgm_fused_kernel": "sgm_fused",
-    "wta_paths_kernel": "wta", "hamming_cost_kernel": "cost", "census9x7_kernel": "census",
+    "sgm_paths_kernel": "sgm_paths",
     "hamming_cost2_kernel": "cost2", "fuse_depth_kernel": "fuse_depth",
     "hamming_cost_rows_kernel": "cost", "census9x7_rows_kernel": "census",
     "census_cost_kernel": "cost", "wta_h_kernel": "wta_h",
