@@ -81,6 +81,11 @@ def parse():
     ap.add_argument("--rehearse-rccl", action="store_true",
                     help="N=1 only: a 1-rank RCCL process group runs the real overlapped "
                          "gather_maps on the comm stream (the N>1 code path on one GPU)")
+    ap.add_argument("--engine", default="auto", choices=["auto", "multi"],
+                    help="auto: --gpus N > 1 without torch.distributed.run drives the N devices "
+                         "from this one process through the C-ABI engine (sva_multi_create + "
+                         "sva_batch_sgm_d, RCCL ncclCommInitAll gather); multi: that engine at "
+                         "any N, N = 1 included")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (real runs); gloo = rehearsal with ranks "
                          "sharing one GPU, maps gathered through host memory")
@@ -686,20 +691,230 @@ def run_array(a, wl, world, rank, local, dev):
         raise SystemExit("multi-rank exchange check failed: " + json.dumps(exchange))
 
 
+def launch_mode(a, env):
+    """How this process runs the N GPUs of a step:
+      'torchrun' -- started by torch.distributed.run (WORLD_SIZE set): one rank
+                    per GPU, torch.distributed (RCCL) gather;
+      'engine'   -- --gpus N > 1 without WORLD_SIZE, or --engine multi: this
+                    process drives devices 0..N-1 through the C-ABI engine
+                    (sva_multi_*), the route a C++ host takes (DESIGN.md §7);
+      'single'   -- one process, one GPU."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in env and world > 1:
+        if world != a.gpus:
+            raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+        if a.engine == "multi":
+            raise SystemExit("--engine multi is one process for all GPUs; do not start it "
+                             "under torch.distributed.run")
+        return "torchrun"
+    if a.engine == "multi" or a.gpus > 1:
+        if a.rehearse_rccl or a.rehearse_overlap or a.dist_backend != "nccl":
+            raise SystemExit("--rehearse-* / --dist-backend apply to the torchrun route only")
+        return "engine"
+    return "single"
+
+
+def run_engine(a, wl):
+    """--gpus N from ONE process through the C-ABI multi-GPU engine: pair u
+    lives on device u mod N (sva_multi_plan), each device runs its pairs on its
+    own contexts/streams, and sva_batch_sgm_d gathers the u16 disparity maps
+    (and f32 sub-pixel maps) to device 0 with RCCL grouped send/recv on a
+    single-process communicator (ncclCommInitAll).  Array workloads then fuse
+    per reference camera on device 0.  Checked once after the timed region:
+    every gathered map vs a single-context recompute on device 0, and the
+    steps re-timed without the gather (each device's pairs through its own
+    engine contexts) for the exposed gather time."""
+    import torch
+    import stereovisionarray_amd as sva
+    from stereovisionarray_amd import synth
+
+    N = a.gpus
+    ndev = torch.cuda.device_count()
+    if N > ndev:
+        raise SystemExit(f"--gpus {N}: only {ndev} HIP device(s) visible")
+    W, H, D = wl["W"], wl["H"], wl["D"]
+    devs = [torch.device("cuda", d) for d in range(N)]
+    torch.cuda.set_device(0)
+    groups = []
+    if "rig" in wl:
+        grid, pairs, rig_label = rig_of(wl["rig"])
+        kmax = max(synth.pair_step(grid[i], grid[j])[2] for i, j in pairs)
+        dmax = min((D - 1) // kmax, 100)
+        delta = synth.array_delta(H, W, dmax)
+        used = sorted({c for q in pairs for c in q})
+        views_np = dict(zip(used, synth.array_views(H, W, [grid[c] for c in used], delta, seed=7)))
+        units = []
+        for i, j in pairs:
+            sx, sy, _ = synth.pair_step(grid[i], grid[j])
+            units.append((views_np[i], views_np[j],
+                          sva.default_params(D=D, dmin=0, dir=sx, dir_y=sy)))
+        off = 0
+        for i in dict.fromkeys(q[0] for q in pairs):
+            n = sum(1 for q in pairs if q[0] == i)
+            bases = [synth.pair_step(grid[i], grid[j])[2] * ARRAY_PITCH
+                     for (_, j) in pairs[off:off + n]]
+            groups.append((off, n, bases))
+            off += n
+        subpixel = 0
+    else:
+        total = wl.get("total_pairs", N * a.pairs_per_rank)
+        seed0 = 0 if "total_pairs" in wl else 1
+        units = []
+        for u in range(total):
+            L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=seed0 + u)
+            units.append((L, R, sva.default_params(D=D, dmin=0, dir=-1, subpixel=1)))
+        subpixel = 1
+    n_units = len(units)
+    per_dev = -(-n_units // N)
+    S = a.streams if a.streams > 0 else (1 if per_dev == 1 or D == 192 else 2)
+    m = sva.Multi(list(range(N)), streams=S, flags=sva.SVA_MULTI_GATHER_RCCL)
+    ctxs = [m.context(d, s) for d in range(N) for s in range(S)]
+    for c in ctxs:
+        c.reserve(W, H, D)
+    dl, dr = [], []
+    for u, (L, R, _) in enumerate(units):
+        dl.append(torch.from_numpy(L).to(devs[u % N]))
+        dr.append(torch.from_numpy(R).to(devs[u % N]))
+    jobs = [(dl[u].data_ptr(), dr[u].data_ptr(), units[u][2]) for u in range(n_units)]
+    maps = torch.zeros((n_units, H, W), dtype=torch.int16, device=devs[0])
+    sub = torch.zeros((n_units, H, W), dtype=torch.float32, device=devs[0]) if subpixel else None
+    depth = torch.zeros((max(len(groups), 1), H, W), dtype=torch.float64, device=devs[0])
+    nvalid = torch.zeros((max(len(groups), 1), H, W), dtype=torch.uint8, device=devs[0])
+    fctx = m.context(0, 0)                 # device 0, stream 0: where the gathered maps land
+
+    def step():
+        m.batch_sgm_d(jobs, W, H, W, maps.data_ptr(), sub.data_ptr() if sub is not None else None)
+        for g, (o, n, bases) in enumerate(groups):
+            fctx.fuse_depth_d(maps[o].data_ptr(), n, W, H, bases, ARRAY_F, ARRAY_PS, 0xFFFF,
+                              depth[g].data_ptr(), nvalid[g].data_ptr())
+
+    # compute-only re-timing: every pair on its engine context, no gather
+    local = [torch.zeros((H, W), dtype=torch.int16, device=devs[u % N]) for u in range(n_units)]
+    plan_ctx = [m.context(u % N, (u // N) % S) for u in range(n_units)]
+
+    def step_local():
+        for u in range(n_units):
+            plan_ctx[u].disparity_sgm_d(dl[u].data_ptr(), dr[u].data_ptr(), W, H, W,
+                                        units[u][2], local[u].data_ptr())
+
+    def run(fn, k, timing):
+        for c in ctxs:
+            c.set_timing(timing)
+            c.reset_timing()
+        m.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        m.synchronize()
+        return time.perf_counter() - t0
+
+    run(step, a.warmup, 0)
+    elapsed = run(step, a.steps, 2)                     # SVA_TIMING_PATHS in the timed region
+    timed_k = kernel_table(ctxs)
+    run(step, min(a.steps, 5), 1)                       # every kernel, after the timed region
+    kernels = kernel_table(ctxs)
+    if "sgm_paths" in timed_k:
+        kernels["sgm_paths"] = timed_k["sgm_paths"]
+    for c in ctxs:
+        c.set_timing(0)
+    compute_ms = run(step_local, max(1, min(a.steps, 10)), 0) / max(1, min(a.steps, 10)) * 1e3
+    # every gathered map vs a single-context recompute on device 0
+    check = sva.Context(0)
+    cs = torch.cuda.Stream(devs[0])
+    check.set_stream(cs.cuda_stream)
+    mism = []
+    got = maps.cpu()
+    checked = min(n_units, max(32, N))      # bounded: 32 units, every owner device
+    for u in range(checked):
+        L, R, p = units[u]
+        ref = torch.zeros((H, W), dtype=torch.int16, device=devs[0])
+        Ld, Rd = torch.from_numpy(L).to(devs[0]), torch.from_numpy(R).to(devs[0])
+        torch.cuda.synchronize(devs[0])
+        check.disparity_sgm_d(Ld.data_ptr(), Rd.data_ptr(), W, H, W, p, ref.data_ptr())
+        check.synchronize()
+        if not torch.equal(ref.cpu(), got[u]):
+            mism.append(u)
+    check.close()
+    ms_per_step = elapsed / a.steps * 1e3
+    value = n_units * W * H * D * a.steps / elapsed / 1e6
+    model, nproc, _ = host_cpu()
+    exchange = {"backend": "rccl", "route": "C-ABI engine: sva_multi_create + sva_batch_sgm_d, "
+                "single-process communicator (ncclCommInitAll), grouped ncclSend/ncclRecv to "
+                "device 0", "rccl_ranks": N, "devices": N, "streams_per_device": S,
+                "units_checked": checked, "units_equal_single_context": checked - len(mism),
+                "remote_unit_recomputed": {"unit": 1 % n_units, "owner_device": (1 % n_units) % N,
+                                           "equal": (1 % n_units) not in mism},
+                "ok": not mism,
+                "compute_only_ms_per_step": round(compute_ms, 4),
+                "exposed_gather_ms_per_step": round(ms_per_step - compute_ms, 4),
+                "map_bytes_per_unit": W * H * 2 + (W * H * 4 if subpixel else 0)}
+    if "rig" in wl:
+        metric = (f"Mdisparities/sec (W·H·D/s), camera array ({rig_label}), {W}x{H} D={D}, "
+                  "gather + fuse")
+        work = (f"{a.workload}: {rig_label}, {n_units} pairs {W}x{H} D={D} Mode S along each "
+                "pair's baseline step, gather + per-camera median fusion on device 0")
+    else:
+        metric = ("Mdisparities/sec (W·H·D/s) at 1080p D=128" if a.workload == "1080p_d128"
+                  else f"Mdisparities/sec (W·H·D/s) {a.workload}")
+        work = (f"{W}x{H} D={D} Mode S SGM (census 9x7, Hamming, 8 paths, WTA+subpixel), "
+                f"{n_units} pair(s) per step")
+    out = {
+        "metric": metric,
+        "value": round(value, 1),
+        "unit": "Mdisp/s",
+        "n_gpus": N,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong" if ("total_pairs" in wl or "rig" in wl) else "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic (MT19937 u8 texture" + (", array views)" if "rig" in wl else
+                                                    ", 16-stripe piecewise-constant disparity)"),
+        "config": {"workload": work, "W": W, "H": H, "D": D, "P1": 10, "P2": 120,
+                   "pairs": n_units,
+                   "parallelism": f"pairs sharded over {N} device(s) of one process "
+                                  "(sva_multi engine), RCCL gather to device 0",
+                   "streams_per_rank": S},
+        "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
+        "roofline": roofline_of(kernels, W, H, D, "1080p_d128" if "rig" in wl else a.workload,
+                                overlapped=S > 1),
+        "cpu_baseline": None,
+        "exchange": exchange,
+        "host": f"{model}, nproc {nproc}",
+    }
+    if N == 1 and S == 1 and "rig" not in wl:
+        out["frame_roofline"] = frame_roofline(W, H, D, ms_per_step / n_units)
+    if N == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(W, H, D, a.cpu_threads)
+    if out["roofline"]:
+        out["roofline"]["traffic_source"] = (f"committed profiles/pmc_{a.workload}.json "
+                                             "(live PMC passes run on the single-GPU route)")
+    print(json.dumps(out), flush=True)
+    for c in ctxs:
+        c.close()
+    m.close()
+    if mism:
+        raise SystemExit(f"engine gather check failed for units {mism[:8]}")
+
+
 def main():
     a = parse()
+    mode = launch_mode(a, os.environ)
     import torch
     import torch.distributed as dist
     import stereovisionarray_amd as sva
     from stereovisionarray_amd import dist as sdist
     from stereovisionarray_amd import synth
 
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
+    if mode == "engine":
+        return run_engine(a, WORKLOADS[a.workload])
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
     ndev = torch.cuda.device_count()

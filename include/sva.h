@@ -347,11 +347,13 @@ typedef struct sva_pair_d {
     sva_sgm_params params;
 } sva_pair_d;
 /* Every pair's Mode S map, gathered into maps (device memory on devices[0],
- * [n_jobs][H][W] u16) and, when subpix is non-NULL and params.subpixel is
- * set, the f32 maps into subpix ([n_jobs][H][W] on devices[0]).  Asynchronous:
- * the results are complete on devices[0]'s first stream (stream_index 0)
- * once the call returns SVA_OK and that stream has run; sva_multi_synchronize
- * waits for everything. */
+ * [n_jobs][H][W] u16) and, when subpix is non-NULL, the f32 maps of the jobs
+ * that set params.subpixel into subpix ([n_jobs][H][W] on devices[0]; the
+ * planes of the other jobs are not written).  Asynchronous: the results are
+ * complete on devices[0]'s first stream (stream_index 0) once the call returns
+ * SVA_OK and that stream has run; sva_multi_synchronize waits for everything.
+ * Work the caller queues on that stream after a call (e.g. reading maps) is
+ * ordered before the next call writes maps / subpix. */
 int sva_batch_sgm_d(void* multi, const sva_pair_d* jobs, int n_jobs, int width, int height,
                     size_t pitch, uint16_t* maps, float* subpix);
 
@@ -363,7 +365,8 @@ int sva_batch_sgm_d(void* multi, const sva_pair_d* jobs, int n_jobs, int width, 
  * Uploads run on per-device copy streams and each pair waits only for its two
  * images, so transfers overlap compute; the fused maps download as each group
  * finishes.  depth: host [n_groups][H][W] f64; n_valid (nullable) host u8,
- * same shape; maps (nullable) host [n_pairs][H][W] u16.  Synchronous. */
+ * same shape; maps (nullable) host [n_pairs][H][W] u16.  Synchronous.  The
+ * pairs of one group must share params.invalid (SVA_ERR_INVALID_ARG). */
 typedef struct sva_array_pair {
     int32_t ref;              /* index into images[]: the reference view      */
     int32_t other;            /* index into images[]: the matched view        */

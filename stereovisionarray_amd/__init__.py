@@ -258,11 +258,22 @@ class Context:
             raise SvaError(st, lib.sva_status_string(st).decode())
         self.h = h
         self.device = device
+        self._owned = True
+
+    @classmethod
+    def borrowed(cls, handle: int, device: int):
+        """A non-owning view of a context another owner destroys (e.g. one of
+        a Multi engine's, sva_multi_context)."""
+        c = cls.__new__(cls)
+        c.h = ct.c_void_p(handle)
+        c.device = device
+        c._owned = False
+        return c
 
     def close(self):
-        if self.h:
+        if self.h and self._owned:
             lib.sva_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
@@ -603,6 +614,12 @@ class Multi:
         out = ct.c_void_p()
         self._chk(lib.sva_multi_context(self.h, device_index, stream_index, ct.byref(out)))
         return out.value
+
+    def context(self, device_index: int, stream_index: int) -> "Context":
+        """The engine's context (device_index, stream_index), borrowed (the
+        engine destroys it): kernel timing, or direct per-device calls."""
+        return Context.borrowed(self.context_handle(device_index, stream_index),
+                                self.devices[device_index])
 
     def batch_sgm_d(self, pairs, W, H, pitch, maps, sub=None):
         """pairs: list of (left_ptr, right_ptr, SgmParams) on their owner devices."""

@@ -240,6 +240,24 @@ int run_pairs(Multi* m, const Plan& P, const std::vector<const uint8_t*>& left,
               uint16_t* maps, float* sub) {
     const int n = (int)P.dev.size();
     const size_t np = (size_t)W * H;
+    // 0. maps / sub are the caller's buffers on devices[0]: results of the
+    // previous call are complete on st(0, 0), and the caller may still be
+    // reading them there.  Every stream that writes into maps / sub -- device
+    // 0's other context streams (local jobs) and, with peer copies, each source
+    // device's st(d, 0) -- starts after what is queued on st(0, 0) now.  (The
+    // RCCL receives run on st(0, 0) itself.)
+    {
+        hipEvent_t e0;
+        MHIP(m, ev_on(m, 0, &e0), "event");
+        MHIP(m, hipEventRecord(e0, m->st(0, 0)), "event record");
+        for (int s = 1; s < m->spd; s++)
+            MHIP(m, hipStreamWaitEvent(m->st(0, s), e0, 0), "stream wait");
+        if (m->mode == SVA_MULTI_GATHER_PEER)
+            for (int d = 1; d < m->nd(); d++) {
+                MHIP(m, hipSetDevice(m->devices[d]), "hipSetDevice");
+                MHIP(m, hipStreamWaitEvent(m->st(d, 0), e0, 0), "stream wait");
+            }
+    }
     // 1. slot workspace per context; a context starts after its device's last gather
     std::vector<char> remote(n, 0);
     for (int j = 0; j < n; j++) remote[j] = P.dev[j] != 0 || m->gather_all;
@@ -287,7 +305,13 @@ int run_pairs(Multi* m, const Plan& P, const std::vector<const uint8_t*>& left,
     // 4. gather (maps, then sub-pixel maps)
     int st = gather(m, P, remote, src_map, (uint8_t*)maps, np * 2);
     if (st) return st;
-    if (sub && (st = gather(m, P, remote, src_sub, (uint8_t*)sub, np * 4))) return st;
+    if (sub) {
+        // only jobs that asked for a sub-pixel map have one (sva.h); the
+        // others' planes of `sub` are left untouched, local or remote
+        std::vector<char> remote_sub(remote);
+        for (int j = 0; j < n; j++) remote_sub[j] = remote[j] && prm[j].subpixel != 0;
+        if ((st = gather(m, P, remote_sub, src_sub, (uint8_t*)sub, np * 4))) return st;
+    }
     for (int d = 0; d < m->nd(); d++) {
         MHIP(m, hipSetDevice(m->devices[d]), "hipSetDevice");
         MHIP(m, hipEventRecord(m->gathered[d], m->st(d, 0)), "event record");
@@ -304,7 +328,10 @@ int check_params(const sva_sgm_params& p) {
 
 // ------------------------------------------- host batch (sva_batch_sgm) --
 // One context's share of sva_batch_sgm: jobs i, i + n, ...; two pipeline
-// slots so that upload(j+1) / download(j-1) overlap compute(j).
+// slots so that upload(j+1) / download(j-1) overlap compute(j).  The lane
+// (streams, events, pinned and device staging) lives in the context
+// (Ctx::batch_lane) from its first batch to sva_destroy: hipHostMalloc /
+// hipFree synchronise the device, so a lane per call cost milliseconds.
 struct HostLane {
     Ctx* c = nullptr;
     hipStream_t up = nullptr, dn = nullptr;
@@ -331,7 +358,6 @@ void lane_free(HostLane& L) {
     (void)hipSetDevice(L.c->device);
     if (L.up) (void)hipStreamSynchronize(L.up);
     if (L.dn) (void)hipStreamSynchronize(L.dn);
-    if (L.c->stream) (void)hipStreamSynchronize(L.c->stream);
     for (int b = 0; b < 2; b++) {
         L.in[b].release();
         L.out[b].release();
@@ -353,15 +379,35 @@ int sva_batch_sgm(void** ctxs, int n_ctx, const sva_pair_job* jobs, int n_jobs,
                   const sva_sgm_params* p, int* job_status) {
     if (!ctxs || n_ctx <= 0 || (n_jobs > 0 && !jobs) || n_jobs < 0 || !p)
         return SVA_ERR_INVALID_ARG;
-    for (int i = 0; i < n_ctx; i++)
+    for (int i = 0; i < n_ctx; i++) {
         if (!ctxs[i]) return SVA_ERR_INVALID_ARG;
+        for (int k = 0; k < i; k++)
+            if (ctxs[k] == ctxs[i]) return SVA_ERR_INVALID_ARG;   // a context is not re-entrant
+    }
     std::vector<int> status(n_jobs, SVA_OK);
     std::vector<std::thread> th;
     for (int i = 0; i < n_ctx; i++) {
         th.emplace_back([&, i]() {
-            HostLane L;
-            L.c = static_cast<Ctx*>(ctxs[i]);
-            const int s0 = lane_init(L);
+            Ctx* cx = static_cast<Ctx*>(ctxs[i]);
+            int s0 = SVA_OK;
+            if (!cx->batch_lane) {
+                HostLane* nl = new (std::nothrow) HostLane();
+                if (!nl) {
+                    s0 = SVA_ERR_OUT_OF_MEMORY;
+                } else {
+                    nl->c = cx;
+                    s0 = lane_init(*nl);
+                    cx->batch_lane = std::shared_ptr<void>(nl, [](void* q) {
+                        HostLane* h = static_cast<HostLane*>(q);
+                        lane_free(*h);
+                        delete h;
+                    });
+                    if (s0 != SVA_OK) cx->batch_lane.reset();
+                }
+            }
+            HostLane dummy;
+            HostLane& L = cx->batch_lane ? *static_cast<HostLane*>(cx->batch_lane.get()) : dummy;
+            L.job[0] = L.job[1] = -1;
             // finish job in slot b: wait for its download, copy out of pinned memory
             auto finish = [&](int b) {
                 const int j = L.job[b];
@@ -430,7 +476,6 @@ int sva_batch_sgm(void** ctxs, int n_ctx, const sva_pair_job* jobs, int n_jobs,
             finish(1);
             // pinned input slots are reused only after their upload completed:
             // e_up precedes e_comp precedes e_dn, which finish() waited on
-            lane_free(L);
         });
     }
     for (auto& t : th) t.join();
@@ -619,6 +664,11 @@ int sva_array_depth(void* mp, const uint8_t* const* images, int n_images, int W,
     for (int g = 0; g < n_groups; g++) {
         const int n = group_start[g + 1] - group_start[g];
         if (n <= 0 || n > 32) return m->fail(SVA_ERR_UNSUPPORTED, "groups of 1..32 pairs");
+        // the fusion rejects one `invalid` value per group
+        for (int j = group_start[g] + 1; j < group_start[g + 1]; j++)
+            if (pairs[j].params.invalid != pairs[group_start[g]].params.invalid)
+                return m->fail(SVA_ERR_INVALID_ARG,
+                               "params.invalid differs within group " + std::to_string(g));
     }
     for (int j = 0; j < n_pairs; j++) {
         const sva_array_pair& q = pairs[j];

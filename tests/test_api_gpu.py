@@ -34,7 +34,7 @@ def test_batch_sgm_matches_single_calls(ctx, sva):
             ed, es = ctx.disparity_sgm(L, R, p)
             assert np.array_equal(d, ed) and np.array_equal(s, es)
         with pytest.raises(sva.SvaError):
-            sva.batch_sgm([ctx, ctx2], pairs[:1], sva.default_params(D=50))
+            sva.batch_sgm([ctx, ctx2], pairs[:1], sva.default_params(D=300))
     finally:
         ctx2.close()
 

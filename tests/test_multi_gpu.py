@@ -165,3 +165,170 @@ def test_host_batch_pipelined_with_failing_pair(ctx, sva):
             assert np.array_equal(d, ed) and np.array_equal(s, es), i
     finally:
         ctx2.close()
+
+
+def test_batch_reuse_does_not_overwrite_maps_being_read(ctx, sva, torch_dev):
+    """the caller reads batch 1's maps on the engine's device-0
+    stream 0 while batch 2 is issued without a host sync.  Batch 2's local
+    job on stream (0, 1) must not overwrite maps before that read has run
+    (a spin kernel holds stream 0 back to open the window)."""
+    if not hasattr(torch.cuda, "_sleep"):
+        pytest.skip("torch.cuda._sleep not available")
+    W, H, D, n = 200, 64, 64, 2
+    m = sva.Multi([0], streams=2, flags=sva.SVA_MULTI_GATHER_RCCL)
+    try:
+        s0 = torch.cuda.Stream(torch_dev)
+        m.context(0, 0).set_stream(s0.cuda_stream)    # the engine's stream (0, 0)
+        pa = [synth.stereo_pair(H, W, D, 0, -1, seed=80 + i)[:2] for i in range(n)]
+        pb = [synth.stereo_pair(H, W, D, 0, -1, seed=90 + i)[:2] for i in range(n)]
+        p = sva.default_params(D=D)
+        dev = [[torch.from_numpy(x).to(torch_dev) for x in q] for q in pa + pb]
+        ja = [(dev[j][0].data_ptr(), dev[j][1].data_ptr(), p) for j in range(n)]
+        jb = [(dev[n + j][0].data_ptr(), dev[n + j][1].data_ptr(), p) for j in range(n)]
+        maps = torch.zeros((n, H, W), dtype=torch.int16, device=torch_dev)
+        snap = torch.zeros_like(maps)
+        torch.cuda.synchronize()
+        m.batch_sgm_d(ja, W, H, W, maps.data_ptr())
+        with torch.cuda.stream(s0):
+            torch.cuda._sleep(200_000_000)              # ~0.1 s on stream (0, 0)
+            snap.copy_(maps)                            # the caller's read of batch 1
+        m.batch_sgm_d(jb, W, H, W, maps.data_ptr())
+        m.synchronize()
+        torch.cuda.synchronize()
+        exp_a = np.stack([ctx.disparity_sgm(L, R, p)[0] for L, R in pa])
+        exp_b = np.stack([ctx.disparity_sgm(L, R, p)[0] for L, R in pb])
+        assert np.array_equal(snap.cpu().numpy().view(np.uint16), exp_a)
+        assert np.array_equal(maps.cpu().numpy().view(np.uint16), exp_b)
+    finally:
+        m.close()
+
+
+def test_batch_sub_planes_only_for_subpixel_jobs(ctx, sva, torch_dev):
+    """with sub given, only jobs that set params.subpixel have
+    their sub-pixel plane written (remote jobs included); the others keep the
+    caller's contents instead of stale slot memory."""
+    W, H, D, n = 150, 48, 64, 4
+    m = sva.Multi([0], streams=2, flags=sva.SVA_MULTI_GATHER_RCCL | sva.SVA_MULTI_GATHER_ALL)
+    try:
+        pairs = [synth.stereo_pair(H, W, D, 0, -1, seed=70 + i)[:2] for i in range(n)]
+        dl = [torch.from_numpy(a).to(torch_dev) for a, _ in pairs]
+        dr = [torch.from_numpy(b).to(torch_dev) for _, b in pairs]
+        ps = [sva.default_params(D=D, subpixel=j % 2) for j in range(n)]
+        maps = torch.zeros((n, H, W), dtype=torch.int16, device=torch_dev)
+        sub = torch.full((n, H, W), -3.0, dtype=torch.float32, device=torch_dev)
+        torch.cuda.synchronize()
+        for _ in range(2):                              # the second call reuses the slots
+            m.batch_sgm_d([(dl[j].data_ptr(), dr[j].data_ptr(), ps[j]) for j in range(n)],
+                          W, H, W, maps.data_ptr(), sub.data_ptr())
+            m.synchronize()
+        got = sub.cpu().numpy()
+        for j, (L, R) in enumerate(pairs):
+            if ps[j].subpixel:
+                _, es = ctx.disparity_sgm(L, R, ps[j])
+                assert np.array_equal(got[j].view(np.uint32), es.view(np.uint32)), j
+            else:
+                assert (got[j] == -3.0).all(), j
+    finally:
+        m.close()
+
+
+def test_array_depth_rejects_mixed_invalid_in_group(sva):
+    m = sva.Multi([0], streams=1, flags=sva.SVA_MULTI_GATHER_PEER)
+    try:
+        v = [np.zeros((24, 24), np.uint8)] * 3
+        p0 = sva.default_params(D=64)
+        p1 = sva.default_params(D=64)
+        p1.invalid = 0
+        jobs = [(0, 1, p0, 0.05), (0, 2, p1, 0.05)]
+        with pytest.raises(sva.SvaError) as e:
+            m.array_depth(v, jobs, [0, 2], 0.05, 1e-4)
+        assert e.value.status == sva.SVA_ERR_INVALID_ARG
+    finally:
+        m.close()
+
+
+def test_host_batch_repeated_calls_reuse_lanes(ctx, sva):
+    """sva_batch_sgm keeps each context's pipeline lane between
+    calls; repeated batches stay correct, and one context listed twice is
+    refused (a context is not re-entrant)."""
+    ctx2 = sva.Context(0)
+    try:
+        pairs = [synth.stereo_pair(70, 130, 64, 0, -1, seed=100 + i)[:2] for i in range(5)]
+        p = sva.default_params(D=64, subpixel=1)
+        first = sva.batch_sgm([ctx, ctx2], pairs, p)
+        for _ in range(3):
+            again = sva.batch_sgm([ctx, ctx2], pairs[::-1], p)
+            for (d1, s1), (d2, s2) in zip(first[::-1], again):
+                assert np.array_equal(d1, d2) and np.array_equal(s1, s2)
+        with pytest.raises(sva.SvaError):
+            sva.batch_sgm([ctx, ctx], pairs, p)
+    finally:
+        ctx2.close()
+
+
+# ---- several devices (ADVICE r02): skipped on a one-GPU box ---------------------
+def _devices(sva):
+    n = min(sva.device_count(), 4)
+    if n < 2:
+        pytest.skip("needs >= 2 HIP devices")
+    return list(range(n))
+
+
+@pytest.mark.parametrize("mode", ["rccl", "peer"])
+def test_batch_sgm_d_across_devices(ctx, sva, mode):
+    """Remote jobs on devices[1..], one RCCL group over several communicators
+    from one thread (or peer copies), per-device slots and gather events:
+    every gathered map and sub-pixel map equals the single-context result."""
+    devs = _devices(sva)
+    W, H, D, n = 180, 72, 64, 2 * len(devs) + 1
+    m = sva.Multi(devs, streams=2, flags=flags_of(sva, mode))
+    try:
+        pairs = [synth.stereo_pair(H, W, D, 0, -1, seed=120 + j)[:2] for j in range(n)]
+        owner = [torch.device("cuda", devs[j % len(devs)]) for j in range(n)]
+        dl = [torch.from_numpy(a).to(owner[j]) for j, (a, _) in enumerate(pairs)]
+        dr = [torch.from_numpy(b).to(owner[j]) for j, (_, b) in enumerate(pairs)]
+        p = sva.default_params(D=D, subpixel=1)
+        d0 = torch.device("cuda", devs[0])
+        maps = torch.zeros((n, H, W), dtype=torch.int16, device=d0)
+        sub = torch.zeros((n, H, W), dtype=torch.float32, device=d0)
+        for d in devs:
+            torch.cuda.synchronize(d)
+        for rep in range(2):
+            order = list(range(n)) if rep == 0 else list(range(n))[::-1]
+            m.batch_sgm_d([(dl[j].data_ptr(), dr[j].data_ptr(), p) for j in range(n)], W, H, W,
+                          maps.data_ptr(), sub.data_ptr())
+            m.synchronize()
+            got = maps.cpu().numpy().view(np.uint16)
+            gsub = sub.cpu().numpy()
+            for j in order:
+                ed, es = ctx.disparity_sgm(*pairs[j], p)
+                assert np.array_equal(got[j], ed), (rep, j)
+                assert np.array_equal(gsub[j].view(np.uint32), es.view(np.uint32)), (rep, j)
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("mode", ["rccl", "peer"])
+def test_array_depth_across_devices(sva, oracle, mode):
+    devs = _devices(sva)
+    W, H, D = 160, 128, 64
+    pitch_m, f, ps = 0.05, 0.05, 0.036 / 160
+    grid, pairs, gs = _mini_rig()
+    views = synth.array_views(H, W, grid, synth.array_delta(H, W, 14), seed=4)
+    jobs, omaps = [], []
+    for i, j in pairs:
+        sx, sy, k = synth.pair_step(grid[i], grid[j])
+        jobs.append((i, j, sva.default_params(D=D, dir=sx, dir_y=sy), k * pitch_m))
+        omaps.append(oracle.sgm2(views[i], views[j], D, 0, sx, sy, subpixel=False)[0])
+    m = sva.Multi(devs, streams=2, flags=flags_of(sva, mode))
+    try:
+        depth, nv, maps = m.array_depth(views, jobs, gs, f, ps, want_maps=True)
+    finally:
+        m.close()
+    for j in range(len(pairs)):
+        assert np.array_equal(maps[j], omaps[j]), pairs[j]
+    for g in range(len(gs) - 1):
+        sl = slice(gs[g], gs[g + 1])
+        ez, en = oracle.fuse_depth(np.stack(omaps[sl]), [b for *_, b in jobs[sl]], f, ps)
+        assert np.array_equal(nv[g], en)
+        assert np.array_equal(depth[g].view(np.uint64), ez.view(np.uint64))

@@ -142,6 +142,18 @@ def main():
                     outs[-1] = (outs[-1], torch.sum(subm.view(torch.int32).to(torch.int64)).item())
             if not os.environ.get("AB_NOCHECK"):     # ablation builds compute other values
                 assert len(set(outs)) == 1, outs
+        if a.entry == "sgm" and it == 0:
+            # every variant must produce the same disparities (and sub-pixel map)
+            outs = []
+            for n, lib, h in handles:
+                lib.sva_disparity_sgm_d(h, ct.c_void_p(dL.data_ptr()), ct.c_void_p(dR.data_ptr()),
+                                        W, H, ct.c_size_t(W), ct.byref(p),
+                                        ct.c_void_p(disp.data_ptr()),
+                                        ct.c_void_p(subm.data_ptr()) if a.sub else None)
+                torch.cuda.synchronize()
+                outs.append((disp.cpu().numpy().tobytes(),
+                             subm.cpu().numpy().tobytes() if a.sub else b""))
+            assert all(o == outs[0] for o in outs), "variants disagree on the disparity map"
         if a.entry == "paths" and it == 0:
             # every variant must produce the same volumes
             outs = []
