@@ -37,27 +37,17 @@ __device__ __forceinline__ void store16_nt(uint8_t* p, const unsigned (&o)[4]) {
     __builtin_nontemporal_store((v4u){o[0], o[1], o[2], o[3]}, (v4u*)p);
 }
 
-// 6-bit layout (decoded by sgm_common.h c6_decode): the main
-// dword and extra ushort of one path lane's 8 costs v[0..7].
-__device__ __forceinline__ unsigned c6_main(const unsigned* v) {
-    return v[0] | v[2] << 6 | (v[6] >> 2) << 12 | v[1] << 16 | v[3] << 22 | (v[7] >> 2) << 28;
-}
-__device__ __forceinline__ unsigned c6_extra(const unsigned* v) {
-    return v[4] | (v[6] & 3u) << 6 | v[5] << 8 | (v[7] & 3u) << 14;
-}
-
 // Census word of the pixel whose 9-byte window row starts at byte s of each
 // ring row; `rows[dy+3]` are the dword views of ring rows y-3 .. y+3.
 __device__ __forceinline__ uint64_t census_at(const unsigned* const* rows, int s) {
     return census9x7(rows, s >> 2, (unsigned)(s & 3));
 }
 
-template <int NC, bool C6>
+template <int NC>
 __global__ __launch_bounds__(CC_BLOCK) void census_cost_kernel(
     const uint8_t* __restrict__ left, const uint8_t* __restrict__ right, int W, int H,
     size_t pitch, int dmin, int dir, int rows, int dreal, uint8_t* __restrict__ C) {
     constexpr int D = NC * 16;
-    static_assert(!C6 || NC == 8, "6-bit costs: D = 128");
     constexpr int NW = PXB + D - 1;                      // right census words per row
     constexpr int RW = (NW + 8 + 4 + 3) / 4 * 4;         // right ring row bytes (+ dword overrun)
     constexpr int LW = (PXB + 8 + 4 + 3) / 4 * 4;        // left ring row bytes
@@ -167,23 +157,6 @@ __global__ __launch_bounds__(CC_BLOCK) void census_cost_kernel(
                 for (int cc = 0; cc < NC / 4; cc++) {
                     const int c = c0 + 4 * cc;
                     const uint64_t* src = base + 16 * c;
-                    if constexpr (C6) {
-                        // chunk c = path lanes 2c, 2c+1: main dwords at byte 8c of
-                        // the pixel's 96, extra ushorts at 64 + 4c
-                        unsigned v[16];
-#pragma unroll
-                        for (int i = 0; i < 16; i++) {
-                            const uint64_t w = lc ^ src[i];
-                            v[i] = (border && (w >> 63)) ? 62u : (unsigned)__popcll(w);
-                        }
-                        typedef unsigned v2u __attribute__((ext_vector_type(2)));
-                        uint8_t* px = C + ((size_t)y * W + x) * 96;
-                        __builtin_nontemporal_store((v2u){c6_main(v), c6_main(v + 8)},
-                                                    (v2u*)(px + 8 * c));
-                        __builtin_nontemporal_store(c6_extra(v) | c6_extra(v + 8) << 16,
-                                                    (unsigned*)(px + 64 + 4 * c));
-                        continue;
-                    }
                     unsigned out[4];
                     if (!border) {
 #pragma unroll
@@ -228,25 +201,18 @@ __global__ __launch_bounds__(CC_BLOCK) void census_cost_kernel(
 bool census_cost_supported(int D) { return D == 64 || D == 128 || D == 192 || D == 256; }
 
 hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right, int W, int H,
-                              size_t pitch, int D, int dmin, int dir, uint8_t* C, int dreal,
-                              bool c6) {
+                              size_t pitch, int D, int dmin, int dir, uint8_t* C, int dreal) {
     if (dreal <= 0) dreal = D;
-    if (c6 && (D != 128 || dreal != D)) return hipErrorInvalidValue;
     ScopedKernelTimer t(c, "cost");
     const int rows = tune::kCensusCostRows;
     const int bpr = (W + PXB - 1) / PXB;
     const dim3 grid((unsigned)(bpr * ((H + rows - 1) / rows)));
     const int sd = dir > 0 ? 1 : -1;
     switch (D) {
-        case 64: hipLaunchKernelGGL((census_cost_kernel<4, false>), grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
-        case 128:
-            if (c6)
-                hipLaunchKernelGGL((census_cost_kernel<8, true>), grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C);
-            else
-                hipLaunchKernelGGL((census_cost_kernel<8, false>), grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C);
-            break;
-        case 192: hipLaunchKernelGGL((census_cost_kernel<12, false>), grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
-        case 256: hipLaunchKernelGGL((census_cost_kernel<16, false>), grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
+        case 64: hipLaunchKernelGGL(census_cost_kernel<4>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
+        case 128: hipLaunchKernelGGL(census_cost_kernel<8>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
+        case 192: hipLaunchKernelGGL(census_cost_kernel<12>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
+        case 256: hipLaunchKernelGGL(census_cost_kernel<16>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -3,7 +3,6 @@
 // (wta_h.hip).  DESIGN.md §4.3 / §4.6.
 #pragma once
 
-#include <type_traits>
 #include <utility>
 
 #include "sva_device.h"
@@ -233,52 +232,6 @@ __device__ __forceinline__ void sgm_step(const unsigned (&cw)[DPL / 4], unsigned
     sgm_step_c<DPL>(c, A, m, ow, P1, P2, e);
 }
 
-// ---- 6-bit cost volume -----------------------------------
-// The frame pipeline at D = 128 stores C with 6 bits per disparity: a pixel's
-// 128 costs are 96 bytes, [64 B main | 32 B extra], where path lane k (costs
-// 8k .. 8k+7, c0..c7 below) owns main dword k and extra ushort k:
-//   main  = c0 | c2 << 6 | (c6 >> 2) << 12 | c1 << 16 | c3 << 22 | (c7 >> 2) << 28
-//   extra = c4 | (c6 & 3) << 6 | c5 << 8 | (c7 & 3) << 14
-// so the four u16 pairs (c0,c1) .. (c6,c7) decode in 9 VALU (c6_decode).  The
-// loads are structured-buffer loads (stride 96, index = pixel): one cursor in
-// pixels, the lane's byte offsets are constants.
-constexpr int kC6Stride = 96;
-__device__ unsigned sbuf_load_b32(rsrc_t r, int vindex, int voffset, int soffset,
-                                  int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.i32");
-__device__ unsigned short sbuf_load_b16(rsrc_t r, int vindex, int voffset, int soffset,
-                                        int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.i16");
-
-__device__ __forceinline__ rsrc_t make_rsrc_c6(const void* base, size_t npix) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)kC6Stride,
-                                             (int)(unsigned)npix, 0x00020000);
-}
-
-struct C6Oct {
-    unsigned m, e;
-};
-
-// The extra ushort comes with its neighbour lane's in one aligned dword
-// (sub-dword loads measured slower); lane k's half is picked by the byte
-// selector of the decode's v_perm.
-__device__ __forceinline__ C6Oct c6_load(rsrc_t r, unsigned pix, int k) {
-    C6Oct o;
-    o.m = sbuf_load_b32(r, (int)pix, 4 * k, 0, tune::kCLoadAux);
-    o.e = sbuf_load_b32(r, (int)pix, 64 + 4 * (k >> 1), 0, tune::kCLoadAux);
-    return o;
-}
-
-// v_perm selector of lane k's extra ushort inside its dword: (b0, 0, b1, 0)
-// of the low or the high half.
-__device__ __forceinline__ unsigned c6_esel(int k) { return (k & 1) ? 0x0c030c02u : 0x0c010c00u; }
-
-__device__ __forceinline__ void c6_decode(const C6Oct& w, unsigned (&c)[4], unsigned esel) {
-    const unsigned y = __builtin_amdgcn_perm(0u, w.e, esel);   // (e.b0, 0, e.b1, 0)
-    c[0] = w.m & 0x003f003fu;
-    c[1] = (w.m >> 6) & 0x003f003fu;
-    c[2] = y & 0x003f003fu;
-    c[3] = ((y >> 6) & 0x00030003u) | ((w.m >> 10) & 0x003c003cu);
-}
-
 // Direction table, identical to oracle svo_direction().
 __device__ __forceinline__ void dir_of(int r, int& rx, int& ry) {
     constexpr int T[8][2] = {{1, 0}, {-1, 0}, {0, 1}, {0, -1}, {1, 1}, {-1, -1}, {-1, 1}, {1, -1}};
@@ -299,11 +252,10 @@ template <int DPL> constexpr int pf_v() {
 // One path line over a materialised cost volume C.  CKPT
 // (horizontal lines only): store segment checkpoints to rCK instead of the
 // full L_r line to rL.
-template <int DPL, bool DIAG, int PF, bool CKPT = false, bool C6 = false>
+template <int DPL, bool DIAG, int PF, bool CKPT = false>
 __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& g, int rx, int ry,
                                           int line, int k, rsrc_t rCK) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
-    static_assert(!C6 || DPL == 8, "the 6-bit cost layout is defined for D = 128");
     const int W = g.W, H = g.H, D = g.D;
     const unsigned P1 = (unsigned)g.P1, P2 = (unsigned)g.P2;
     const int steps = ry == 0 ? W : H;
@@ -317,17 +269,8 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
     cc.off = ((unsigned)y0 * (unsigned)W + (unsigned)x0) * (unsigned)D + (unsigned)(k * DPL);
     // Prefetch cursor: runs PF steps ahead and may run past the line's end;
     // those loads land in-range garbage or, past the volume, the buffer range
-    // check returns 0 -- never consumed either way.  With C6 it counts pixels
-    // (structured loads), otherwise bytes of the u8 volume.
+    // check returns 0 -- never consumed either way.
     Cursor<false> pc = cc;
-    const unsigned pstride = C6 ? (unsigned)(ry * W + rx) : stride;
-    const unsigned pWD = C6 ? (unsigned)W : WD;
-    if constexpr (C6) pc.off = (unsigned)y0 * (unsigned)W + (unsigned)x0;
-    using Slot = std::conditional_t<C6, C6Oct, Words<NW>>;
-    auto load_slot = [&](unsigned off) -> Slot {
-        if constexpr (C6) return c6_load(rC, off, k);
-        else return bload<NW>(rC, off);
-    };
     // Diagonal lines wrap without per-step x tracking.  Line l visits
     // x = (l + rx*t) mod W and wraps between pixels s and s+1 when s + 1 =
     // W - l (rx = +1) or l + 1 (rx = -1), then every W steps: tw* hold each
@@ -352,15 +295,15 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
     unsigned m = 0u;
     Edges edges;
 
-    Slot ring[PF];
+    Words<NW> ring[PF];
 #pragma unroll
     for (int p = 0; p < PF; p++) {
-        ring[p] = load_slot(pc.off);
-        pc.off += pstride;
+        ring[p] = bload<NW>(rC, pc.off);
+        pc.off += stride;
         if constexpr (DIAG) {   // the advance past pixel PF-1 is checked by step 0
             if (p < PF - 1) {
                 const bool w = p + 1 == twp;
-                const unsigned fixed = rx > 0 ? pc.off - pWD : pc.off + pWD;
+                const unsigned fixed = rx > 0 ? pc.off - WD : pc.off + WD;
                 pc.off = w ? fixed : pc.off;
                 twp = w ? twp + W : twp;
             }
@@ -376,17 +319,11 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
     // every wait is for a load issued ~PF steps earlier.  (Refilling first
     // made hipcc copy the whole ring at the loop head behind vmcnt(1..3).)
     auto step = [&](int p, bool refill, int ts) {
-        unsigned ow[NW];
-        if constexpr (C6) {
-            unsigned c[NP];
-            c6_decode(ring[p], c, c6_esel(k));
-            sgm_step_c<DPL>(c, A, m, ow, P1, P2, edges);
-        } else {
-            unsigned cw[NW];
+        unsigned cw[NW];
 #pragma unroll
-            for (int w = 0; w < NW; w++) cw[w] = ring[p].w[w];
-            sgm_step<DPL>(cw, A, m, ow, P1, P2, edges);
-        }
+        for (int w = 0; w < NW; w++) cw[w] = ring[p].w[w];
+        unsigned ow[NW];
+        sgm_step<DPL>(cw, A, m, ow, P1, P2, edges);
         if constexpr (CKPT) {
             // ts is the (wave-uniform) step index; x the pixel just computed
             const int x = rx > 0 ? ts : W - 1 - ts;
@@ -422,7 +359,7 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
                 }
                 if (pev) {
                     const bool wrapped = ts + PF == twp;
-                    const unsigned fixed = rx > 0 ? pc.off - pWD : pc.off + pWD;
+                    const unsigned fixed = rx > 0 ? pc.off - WD : pc.off + WD;
                     pc.off = wrapped ? fixed : pc.off;
                     twp = wrapped ? twp + W : twp;
                     if (ep == 3) Tp += W;
@@ -431,8 +368,8 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
         }
         if (refill) {
             __builtin_amdgcn_sched_barrier(0);
-            ring[p] = load_slot(pc.off);
-            pc.off += pstride;               // wrap corrected by the next step
+            ring[p] = bload<NW>(rC, pc.off);
+            pc.off += stride;                // wrap corrected by the next step
             __builtin_amdgcn_sched_barrier(0);
         }
     };

@@ -32,7 +32,6 @@
 //      horizontal ones store only segment checkpoints, [2][H][ns][D], and
 //      wta_h.hip recomputes them per segment: 8 C reads + 6 L writes.
 #include "sgm_common.h"
-#include "sva_tuning.h"
 
 namespace sva {
 namespace {
@@ -42,7 +41,7 @@ using namespace sgm;
 constexpr int PATH_BLOCK = 256;
 constexpr int LINES_PER_BLOCK = PATH_BLOCK / 16;
 
-template <int DPL, bool C6>
+template <int DPL>
 __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __restrict__ C,
                                                                uint8_t* __restrict__ L8,
                                                                uint8_t* __restrict__ CK,
@@ -65,20 +64,20 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
     if (line >= nlines) return;  // whole 16-lane row leaves together
     int rx, ry;
     dir_of(r, rx, ry);
-    const rsrc_t rC = C6 ? make_rsrc_c6(C, (size_t)g.W * g.H) : make_rsrc(C, g.vol);
+    const rsrc_t rC = make_rsrc(C, g.vol);
     const int slot = g.ckpt ? r - 2 : r;
     if (r >= 4) {
         const rsrc_t rL = make_rsrc(L8 + (size_t)slot * g.vol, g.vol);
-        path_line<DPL, true, pf_v<DPL>(), false, C6>(rC, rL, g, rx, ry, line, k, rL);
+        path_line<DPL, true, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
     } else if (r >= 2) {
         const rsrc_t rL = make_rsrc(L8 + (size_t)slot * g.vol, g.vol);
-        path_line<DPL, false, pf_v<DPL>(), false, C6>(rC, rL, g, rx, ry, line, k, rL);
+        path_line<DPL, false, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
     } else if (g.ckpt) {
         const rsrc_t rCK = make_rsrc(CK + (size_t)r * g.ckvol, g.ckvol);
-        path_line<DPL, false, pf_h<DPL>(), true, C6>(rC, rC, g, rx, ry, line, k, rCK);
+        path_line<DPL, false, pf_h<DPL>(), true>(rC, rC, g, rx, ry, line, k, rCK);
     } else {
         const rsrc_t rL = make_rsrc(L8 + (size_t)r * g.vol, g.vol);
-        path_line<DPL, false, pf_h<DPL>(), false, C6>(rC, rL, g, rx, ry, line, k, rL);
+        path_line<DPL, false, pf_h<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
     }
 }
 
@@ -91,8 +90,7 @@ int sgm_seg_log2(int D) { return seg_log2_of(D); }
 int ckpt_segments(int W, int D) { return (W + (1 << seg_log2_of(D)) - 1) >> seg_log2_of(D); }
 
 hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
-                        uint8_t* L8, uint8_t* CK, bool c6) {
-    if (c6 && D != 128) return hipErrorInvalidValue;
+                        uint8_t* L8, uint8_t* CK) {
     DispatchTimer t(c, "sgm_paths");
     PathGeom g;
     g.W = W; g.H = H; g.D = D; g.P1 = P1; g.P2 = P2;
@@ -104,19 +102,15 @@ hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, i
     g.ckvol = (size_t)H * g.ns * D;
     if (g.vol >= (size_t)1 << 32) return hipErrorInvalidValue;  // 32-bit buffer offsets
     dim3 grid(2 * g.blk_h + 6 * g.blk_w);
-#define SVA_PATHS_LAUNCH(DPL_, C6_)                                                          \
-    hipExtLaunchKernelGGL((sgm_paths_kernel<DPL_, C6_>), grid, dim3(PATH_BLOCK),                \
-                          (size_t)tune::kPathsLdsPad, c.stream,                                 \
-                          t.start, t.stop, 0, C, L8, CK, g);                                    \
+#define SVA_PATHS_LAUNCH(DPL_)                                                               \
+    hipExtLaunchKernelGGL(sgm_paths_kernel<DPL_>, grid, dim3(PATH_BLOCK), 0, c.stream, t.start, \
+                          t.stop, 0, C, L8, CK, g);                                    \
     t.used = true
     switch (D) {
-        case 64: SVA_PATHS_LAUNCH(4, false); break;
-        case 128:
-            if (c6) { SVA_PATHS_LAUNCH(8, true); }
-            else { SVA_PATHS_LAUNCH(8, false); }
-            break;
-        case 192: SVA_PATHS_LAUNCH(12, false); break;
-        case 256: SVA_PATHS_LAUNCH(16, false); break;
+        case 64: SVA_PATHS_LAUNCH(4); break;
+        case 128: SVA_PATHS_LAUNCH(8); break;
+        case 192: SVA_PATHS_LAUNCH(12); break;
+        case 256: SVA_PATHS_LAUNCH(16); break;
         default: return hipErrorInvalidValue;
     }
 #undef SVA_PATHS_LAUNCH

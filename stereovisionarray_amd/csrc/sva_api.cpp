@@ -16,7 +16,6 @@
 #include <vector>
 
 #include "sva_internal.h"
-#include "sva_tuning.h"
 
 using namespace sva;
 
@@ -174,14 +173,14 @@ size_t ckpt_bytes(int W, int H, int D) { return 2 * (size_t)H * ckpt_segments(W,
 // recomputes the two horizontal directions per segment and picks d*.  Dp is
 // the native volume width, p->D <= Dp the caller's disparities (§4.7).
 int paths_wta(Ctx* c, const uint8_t* C, int W, int H, const sva_sgm_params* p, int Dp,
-              uint16_t* disp, float* sub, bool c6 = false) {
+              uint16_t* disp, float* sub) {
     const size_t nv = (size_t)W * H * (size_t)Dp;
     SVA_HIP(c, c->paths.ensure(nv * 6), "path workspace");
     SVA_HIP(c, c->ckpt.ensure(ckpt_bytes(W, H, Dp)), "checkpoint workspace");
     uint8_t* L6 = (uint8_t*)c->paths.ptr;
     uint8_t* CK = (uint8_t*)c->ckpt.ptr;
-    SVA_HIP(c, launch_paths(*c, C, W, H, Dp, p->P1, p->P2, L6, CK, c6), "paths launch");
-    SVA_HIP(c, launch_wta_h(*c, C, L6, CK, W, H, Dp, p->P1, p->P2, p->dmin, disp, sub, p->D, c6),
+    SVA_HIP(c, launch_paths(*c, C, W, H, Dp, p->P1, p->P2, L6, CK), "paths launch");
+    SVA_HIP(c, launch_wta_h(*c, C, L6, CK, W, H, Dp, p->P1, p->P2, p->dmin, disp, sub, p->D),
             "wta launch");
     return SVA_OK;
 }
@@ -206,18 +205,15 @@ int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int
         // once per matching role when the L/R check runs.
         // In-process A/B per frame at 1080p: D=128 1.129 -> 1.112 ms,
         // D=192 1.646 -> 1.588 ms; D=64 is faster split (0.609 vs 0.650 ms).
-        // D = 128 exactly: the 6-bit cost layout.
-        const bool c6 = tune::kCostPack6 == 1 && Dp == 128 && p->D == 128;
-        SVA_HIP(c, launch_census_cost(*c, left, right, W, H, pitch, Dp, p->dmin, p->dir, C, p->D,
-                                      c6),
+        SVA_HIP(c, launch_census_cost(*c, left, right, W, H, pitch, Dp, p->dmin, p->dir, C, p->D),
                 "cost launch");
-        if ((s = paths_wta(c, C, W, H, p, Dp, disp, sub, c6))) return s;
+        if ((s = paths_wta(c, C, W, H, p, Dp, disp, sub))) return s;
         if (p->lr_check) {
             // right image as reference: the images swap roles, the step flips
             SVA_HIP(c, launch_census_cost(*c, right, left, W, H, pitch, Dp, p->dmin, -p->dir, C,
-                                          p->D, c6),
+                                          p->D),
                     "cost launch");
-            if ((s = paths_wta(c, C, W, H, p, Dp, dr, nullptr, c6))) return s;
+            if ((s = paths_wta(c, C, W, H, p, Dp, dr, nullptr))) return s;
             SVA_HIP(c, launch_lr_check(*c, disp, dr, sub, W, H, p->dir, 0, p->lr_max_diff,
                                        p->invalid),
                     "lr launch");
@@ -598,9 +594,7 @@ int sva_paths_ckpt_d(void* ctx, const uint8_t* C, int W, int H, const sva_sgm_pa
     int s;
     if ((s = check_sgm(c, p, W, H, true))) return s;
     if (!C || !L6 || !CK || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
-    SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L6, CK,
-                            tune::kCostPack6 == 2 && p->D == 128),   // timing probe only
-            "paths launch");
+    SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L6, CK), "paths launch");
     return SVA_OK;
 }
 

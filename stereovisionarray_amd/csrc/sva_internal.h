@@ -126,16 +126,14 @@ bool census_cost_supported(int D);
 // D is the native volume width (64/128/192/256); dreal <= D the caller's
 // disparity count: d >= dreal gets cost 255 (0 = D).
 hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right, int W, int H,
-                              size_t pitch, int D, int dmin, int dir, uint8_t* C, int dreal = 0,
-                              bool c6 = false);
+                              size_t pitch, int D, int dmin, int dir, uint8_t* C, int dreal = 0);
 hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,
                        int dmin, int dir, uint8_t* C, int dreal = 0);
 // sgm_paths.hip -- all 8 directions in one launch.  CK == nullptr: L8 =
 // [8][H][W][D] u8.  CK set (checkpoint mode): L8 = [6][H][W][D]
 // (directions 2..7) and CK = [2][H][ckpt_segments(W, D)][D] horizontal states.
-// c6: C is the 6-bit cost layout of DESIGN.md §4.8 (D = 128 only).
 hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
-                        uint8_t* L8, uint8_t* CK = nullptr, bool c6 = false);
+                        uint8_t* L8, uint8_t* CK = nullptr);
 bool paths_supported(int D);
 // Native volume width of a frame with D disparities: 64, 128, 192 or 256
 // (the smallest >= D), 0 when D is outside 1..256.
@@ -148,7 +146,7 @@ int sgm_seg_log2(int D);
 // dreal < D: a padded frame, WTA over d < dreal only.
 hipError_t launch_wta_h(Ctx& c, const uint8_t* C, const uint8_t* L6, const uint8_t* CK, int W,
                         int H, int D, int P1, int P2, int dmin, uint16_t* disp, float* sub,
-                        int dreal = 0, bool c6 = false);
+                        int dreal = 0);
 // wta.hip
 hipError_t launch_sum(Ctx& c, const uint8_t* L8, int W, int H, int D, uint16_t* S);
 hipError_t launch_wta_from_sum(Ctx& c, const uint16_t* S, int W, int H, int D, int dmin,

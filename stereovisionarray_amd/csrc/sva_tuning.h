@@ -27,12 +27,6 @@ constexpr int kPfH16 = 12, kPfV16 = 8;
 // Cache-policy bits of the cost-volume loads.  A/B (full frame, in-process):
 // nt (2) +8 %, sc0+nt (3) +8 %; sc0 (1), sc0+sc1 (17), 8, 16 within noise.
 constexpr int kCLoadAux = 0;
-// 6-bit cost volume at D = 128: probe switch of the round-3
-// A/B, read by the frame pipeline.
-constexpr int kCostPack6 = 0;
-// Dynamic LDS per path-kernel workgroup (bytes); nonzero only to cap
-// occupancy in experiments (e.g. 41 KB -> 3 workgroups per CU).
-constexpr int kPathsLdsPad = 0;
 
 // ---- wta_h.hip --------------------------------------------
 // Prefetch depth (steps) of the forward pass (1 cost load per step) and the

@@ -85,7 +85,7 @@ __device__ __forceinline__ void load_state(rsrc_t r, unsigned off, unsigned (&A)
     m = row_min_u32(mm);
 }
 
-template <int DPL, bool PAD, bool C6>
+template <int DPL, bool PAD>
 __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C,
                                                    const uint8_t* __restrict__ L6,
                                                    const uint8_t* __restrict__ CK, WtaHGeom g,
@@ -104,9 +104,7 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
     const int n = W - x0 < K ? W - x0 : K;     // pixels in this segment (uniform)
     const unsigned uD = (unsigned)D;
     const unsigned base = (unsigned)y * (unsigned)W * uD + (unsigned)(k * DPL);   // (0, y)
-    static_assert(!C6 || (DPL == 8 && !PAD), "6-bit costs: D = 128, no padding");
-    const rsrc_t rC = C6 ? make_rsrc_c6(C, (size_t)g.W * g.H) : make_rsrc(C, g.vol);
-    const unsigned pix0 = (unsigned)y * (unsigned)W;                                  // (0, y)
+    const rsrc_t rC = make_rsrc(C, g.vol);
     const rsrc_t rCK0 = make_rsrc(CK, g.ckvol);
     const rsrc_t rCK1 = make_rsrc(CK + g.ckvol, g.ckvol);
     rsrc_t rV[6];
@@ -137,43 +135,24 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
     // The forward pass keeps the segment's cost words for the backward pass in
     // LDS, lane-major per (pixel, word) so that accesses are conflict-free:
     // re-reading C instead cost 2-5 % (it came from HBM a second time at D > 128).
-    // 6-bit costs (C6) keep the main dword and the extra ushort: 48 KB at
-    // D = 128 instead of 64 KB, 3 workgroups per CU instead of 2.
-    constexpr int CW = C6 ? 1 : NW;                      // dwords per (pixel, lane)
-    __shared__ unsigned cseg[K * CW * HB];
-    __shared__ unsigned short cseg_e[C6 ? K * HB : 1];
+    __shared__ unsigned cseg[K * NW * HB];
     const int tid = (int)threadIdx.x;
     unsigned LR[K][NW];
-    using Slot = std::conditional_t<C6, C6Oct, Words<NW>>;
-    auto load1 = [&](int j) -> Slot {
-        if constexpr (C6) return c6_load(rC, pix0 + (unsigned)(x0 + j), k);
-        else return bload<NW>(rC, base + (unsigned)(x0 + j) * uD);
-    };
-    Slot r1[PF1];
+    Words<NW> r1[PF1];
 #pragma unroll
-    for (int p = 0; p < PF1; p++) r1[p] = load1(p);
+    for (int p = 0; p < PF1; p++) r1[p] = bload<NW>(rC, base + (unsigned)(x0 + p) * uD);
     for_seq<K>([&](auto J) {
         constexpr int j = decltype(J)::value;
         constexpr int slot = j % PF1;
-        if constexpr (C6) {
-            cseg[j * HB + tid] = r1[slot].m;
-            cseg_e[j * HB + tid] = (unsigned short)(r1[slot].e >> (16 * (k & 1)));
-            if (j < n) {
-                unsigned c[NP];
-                c6_decode(r1[slot], c, c6_esel(k));
-                sgm_step_c<DPL>(c, A, m, LR[j], P1, P2, edges);
-            }
-        } else {
-            unsigned cw[NW];
+        unsigned cw[NW];
 #pragma unroll
-            for (int w = 0; w < NW; w++) cw[w] = r1[slot].w[w];
+        for (int w = 0; w < NW; w++) cw[w] = r1[slot].w[w];
 #pragma unroll
-            for (int w = 0; w < NW; w++) cseg[(j * NW + w) * HB + tid] = cw[w];
-            if (j < n) sgm_step<DPL>(cw, A, m, LR[j], P1, P2, edges);
-        }
+        for (int w = 0; w < NW; w++) cseg[(j * NW + w) * HB + tid] = cw[w];
+        if (j < n) sgm_step<DPL>(cw, A, m, LR[j], P1, P2, edges);
         if constexpr (j + PF1 < K) {
             __builtin_amdgcn_sched_barrier(0);
-            r1[slot] = load1(j + PF1);
+            r1[slot] = bload<NW>(rC, base + (unsigned)(x0 + j + PF1) * uD);
             __builtin_amdgcn_sched_barrier(0);
         }
     });
@@ -206,20 +185,10 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
         constexpr int j = K - 1 - q;
         constexpr int slot = q % PF2;
         if (j < n) {
-            unsigned ow[NW];
-            if constexpr (C6) {
-                C6Oct w;
-                w.m = cseg[j * HB + tid];
-                w.e = cseg_e[j * HB + tid];
-                unsigned c[NP];
-                c6_decode(w, c, 0x0c010c00u);
-                sgm_step_c<DPL>(c, A, m, ow, P1, P2, edges);
-            } else {
-                unsigned cw[NW];
+            unsigned cw[NW], ow[NW];
 #pragma unroll
-                for (int w = 0; w < NW; w++) cw[w] = cseg[(j * NW + w) * HB + tid];
-                sgm_step<DPL>(cw, A, m, ow, P1, P2, edges);
-            }
+            for (int w = 0; w < NW; w++) cw[w] = cseg[(j * NW + w) * HB + tid];
+            sgm_step<DPL>(cw, A, m, ow, P1, P2, edges);
             unsigned S[NP];
 #pragma unroll
             for (int p = 0; p < NP; p++) S[p] = A[p];      // L_1 (u16 pairs, < 256)
@@ -263,13 +232,12 @@ bool wta_h_supported(int D) { return D == 64 || D == 128 || D == 192 || D == 256
 
 hipError_t launch_wta_h(Ctx& c, const uint8_t* C, const uint8_t* L6, const uint8_t* CK, int W,
                         int H, int D, int P1, int P2, int dmin, uint16_t* disp, float* sub,
-                        int dreal, bool c6) {
+                        int dreal) {
     ScopedKernelTimer t(c, "wta_h");
     WtaHGeom g;
     g.W = W; g.H = H; g.D = D; g.P1 = P1; g.P2 = P2; g.dmin = dmin;
     g.dreal = dreal > 0 && dreal < D ? dreal : D;
     const bool pad = g.dreal < D;
-    if (c6 && (D != 128 || pad)) return hipErrorInvalidValue;
     g.ns = ckpt_segments(W, D);
     const size_t vol = (size_t)W * H * D;
     if (vol >= (size_t)1 << 32) return hipErrorInvalidValue;
@@ -278,20 +246,14 @@ hipError_t launch_wta_h(Ctx& c, const uint8_t* C, const uint8_t* L6, const uint8
     const dim3 grid((unsigned)(g.ns * ((H + HROWS - 1) / HROWS)));
 #define SVA_WTAH(DPL_)                                                                          \
     if (pad)                                                                                    \
-        hipLaunchKernelGGL((wta_h_kernel<DPL_, true, false>), grid, dim3(HB), 0, c.stream, C,   \
-                           L6, CK, g, disp, sub);                                               \
+        hipLaunchKernelGGL((wta_h_kernel<DPL_, true>), grid, dim3(HB), 0, c.stream, C, L6, CK,  \
+                           g, disp, sub);                                                       \
     else                                                                                        \
-        hipLaunchKernelGGL((wta_h_kernel<DPL_, false, false>), grid, dim3(HB), 0, c.stream, C,  \
-                           L6, CK, g, disp, sub)
+        hipLaunchKernelGGL((wta_h_kernel<DPL_, false>), grid, dim3(HB), 0, c.stream, C, L6, CK, \
+                           g, disp, sub)
     switch (D) {
         case 64: SVA_WTAH(4); break;
-        case 128:
-            if (c6)
-                hipLaunchKernelGGL((wta_h_kernel<8, false, true>), grid, dim3(HB), 0, c.stream, C,
-                                   L6, CK, g, disp, sub);
-            else
-                SVA_WTAH(8);
-            break;
+        case 128: SVA_WTAH(8); break;
         case 192: SVA_WTAH(12); break;
         case 256: SVA_WTAH(16); break;
         default: return hipErrorInvalidValue;
