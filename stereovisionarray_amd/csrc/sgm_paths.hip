@@ -32,6 +32,7 @@
 //      horizontal ones store only segment checkpoints, [2][H][ns][D], and
 //      wta_h.hip recomputes them per segment: 8 C reads + 6 L writes.
 #include "sgm_common.h"
+#include "sva_tuning.h"
 
 namespace sva {
 namespace {
@@ -54,9 +55,17 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
         lb = b - r * g.blk_h;
         __builtin_amdgcn_s_setprio(1);
     } else {
+        // band-major: the six vertical / diagonal directions of a 16-line band
+        // are adjacent in dispatch order, so the waves that read a cost row
+        // (its vertical band and the diagonal bands crossing it) start
+        // together and progress at a similar pace: more of the second and
+        // third reads of a row come from the caches.  A/B in-process at 1080p
+        // D=128 (profiles/r03_v3): kernel 0.616-0.622 -> 0.594-0.599 ms, frame
+        // 261-263K -> 266-267K Mdisp/s; direction-major had the first-dispatched
+        // direction hundreds of steps ahead.
         b -= 2 * g.blk_h;
-        r = 2 + b / g.blk_w;
-        lb = b - (r - 2) * g.blk_w;
+        r = 2 + b % 6;
+        lb = b / 6;
     }
     const int line = lb * LINES_PER_BLOCK + (threadIdx.x >> 4);
     const int k = threadIdx.x & 15;
