@@ -34,7 +34,10 @@ constexpr uint64_t kOutsideCC = 1ull << 63;   // never set in a census word (bit
 
 __device__ __forceinline__ void store16_nt(uint8_t* p, const unsigned (&o)[4]) {
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
-    __builtin_nontemporal_store((v4u){o[0], o[1], o[2], o[3]}, (v4u*)p);
+    if constexpr (tune::kCostStoreNT)
+        __builtin_nontemporal_store((v4u){o[0], o[1], o[2], o[3]}, (v4u*)p);
+    else
+        *(v4u*)p = (v4u){o[0], o[1], o[2], o[3]};
 }
 
 // Census word of the pixel whose 9-byte window row starts at byte s of each

@@ -35,6 +35,9 @@ constexpr int kCLoadAux = 0;
 // D=256 -2.4 %; deeper at D=128, 6 or 8, within noise).
 constexpr int kWtahPfFwd = 8, kWtahPfBwd = 4;
 constexpr int kWtahPfFwdWide = 4, kWtahPfBwdWide = 4;
+// Pixels of a segment whose cost words wta_h keeps in LDS for the backward
+// pass (0 = the whole segment); the others are re-read from global memory.
+constexpr int kWtahLdsPix = 0;
 
 // ---- census.hip / census_cost.hip / cost.hip ------------
 // Rows per workgroup of the multi-row census kernel.
@@ -45,6 +48,8 @@ constexpr int kCensusRows = 16;
 // 0.093 / 0.101 ms in round 2.
 constexpr int kCensusCostPx = 128;
 constexpr int kCensusCostRows = 4;
+// Cost-volume stores of census_cost: 1 non-temporal, 0 default policy.
+constexpr int kCostStoreNT = 1;
 
 // ---- refpath.hip, Mode R plane kernel v3 ------------------
 constexpr int kPlaneOuKB = 24;      // staged O chunk (KB)

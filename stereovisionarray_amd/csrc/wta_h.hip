@@ -23,6 +23,7 @@
 // the path kernel writes 6 volumes instead of 8.
 #include "sgm_common.h"
 #include "wta_common.h"
+#include "sva_tuning.h"
 
 namespace sva {
 namespace {
@@ -135,7 +136,11 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
     // The forward pass keeps the segment's cost words for the backward pass in
     // LDS, lane-major per (pixel, word) so that accesses are conflict-free:
     // re-reading C instead cost 2-5 % (it came from HBM a second time at D > 128).
-    __shared__ unsigned cseg[K * NW * HB];
+    // pixels [0, KL) of the segment keep their cost words in LDS; the rest
+    // (read late by the forward pass, early by the backward one) are re-read
+    // from global memory, where they are still cached (tune::kWtahLdsPix)
+    constexpr int KL = tune::kWtahLdsPix > 0 && tune::kWtahLdsPix < K ? tune::kWtahLdsPix : K;
+    __shared__ unsigned cseg[KL * NW * HB];
     const int tid = (int)threadIdx.x;
     unsigned LR[K][NW];
     Words<NW> r1[PF1];
@@ -148,7 +153,8 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
 #pragma unroll
         for (int w = 0; w < NW; w++) cw[w] = r1[slot].w[w];
 #pragma unroll
-        for (int w = 0; w < NW; w++) cseg[(j * NW + w) * HB + tid] = cw[w];
+        for (int w = 0; w < NW; w++)
+            if constexpr (j < KL) cseg[(j * NW + w) * HB + tid] = cw[w];
         if (j < n) sgm_step<DPL>(cw, A, m, LR[j], P1, P2, edges);
         if constexpr (j + PF1 < K) {
             __builtin_amdgcn_sched_barrier(0);
@@ -167,10 +173,14 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
         m = 0u;
     }
     Words<NW> rv[PF2][6];
+    Words<NW> rc[KL < K ? PF2 : 1];
     auto issue = [&](int slot, int j) {
         const unsigned off = base + (unsigned)(x0 + j) * uD;
 #pragma unroll
         for (int r = 0; r < 6; r++) rv[slot][r] = bload<NW, vol_aux<DPL>()>(rV[r], off);
+        if constexpr (KL < K) {
+            if (j >= KL) rc[slot] = bload<NW>(rC, off);
+        }
     };
 #pragma unroll
     for (int q = 0; q < PF2; q++) issue(q, K - 1 - q);
@@ -187,7 +197,10 @@ __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C
         if (j < n) {
             unsigned cw[NW], ow[NW];
 #pragma unroll
-            for (int w = 0; w < NW; w++) cw[w] = cseg[(j * NW + w) * HB + tid];
+            for (int w = 0; w < NW; w++) {
+                if constexpr (j < KL) cw[w] = cseg[(j * NW + w) * HB + tid];
+                else cw[w] = rc[KL < K ? slot : 0].w[w];
+            }
             sgm_step<DPL>(cw, A, m, ow, P1, P2, edges);
             unsigned S[NP];
 #pragma unroll
