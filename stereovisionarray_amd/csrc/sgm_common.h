@@ -330,8 +330,8 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
             constexpr int SL = seg_log2<DPL>(), SEG = 1 << SL;
             const bool hit = rx > 0 ? (((x + 1) & (SEG - 1)) == 0 && x + 1 < W)
                                     : ((x & (SEG - 1)) == 0 && x > 0);
-            if (hit)   // default policy: the WTA kernel reads these back soon
-                bstore<NW, 0>(rCK, ((unsigned)(y0 * g.ns + (x >> SL)) * (unsigned)D +
+            if (hit)   // default policy (tune::kCkptStoreAux): the WTA kernel reads these back soon
+                bstore<NW, tune::kCkptStoreAux>(rCK, ((unsigned)(y0 * g.ns + (x >> SL)) * (unsigned)D +
                                          (unsigned)(k * DPL)), ow);
         } else {
             bstore<NW>(rL, cc.off, ow);

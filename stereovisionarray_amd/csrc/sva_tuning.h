@@ -17,7 +17,9 @@ namespace tune {
 // In-process A/B (tools/ab_paths.py): 1080p D=128 H/V 8/8 0.755-0.788 ms,
 // 32/12 0.661 (149 VGPRs, 3 waves/SIMD), 40/8 0.689 (2 waves/SIMD), 32/4
 // 0.770; re-checked after the round-2 step changes: 32/12 0.597, 32/16 0.596,
-// 32/8 0.601, 28/12 0.597, 36/12 0.599.  D=64 (1080p) 40/12 0.372 vs 8/8
+// 32/8 0.601, 28/12 0.597, 36/12 0.599; after the band-major dispatch (round
+// 3, profiles/r03_v6) 32/12 0.5845, 32/16 0.5834, 32/8 0.5875, 28/12 0.5815,
+// 36/12 0.5798 (frames 0.952-0.966 ms, all within noise).  D=64 (1080p) 40/12 0.372 vs 8/8
 // 0.416; D=192 24/8 0.996 vs 12/8 1.154; D=256 (4K) 12/8 (16/8 equal, 20/8
 // and 12/12 +3 %).
 constexpr int kPfH4 = 40, kPfV4 = 12;
@@ -27,6 +29,10 @@ constexpr int kPfH16 = 12, kPfV16 = 8;
 // Cache-policy bits of the cost-volume loads.  A/B (full frame, in-process):
 // nt (2) +8 %, sc0+nt (3) +8 %; sc0 (1), sc0+sc1 (17), 8, 16 within noise.
 constexpr int kCLoadAux = 0;
+// Cache-policy bits of the horizontal checkpoint stores (0 = default: wta_h
+// reads them back soon).  nt (2) measured: frame 0.952 vs 0.963 ms median,
+// min 0.948 vs 0.942 -- noise (profiles/r03_v6/ab_retune_sgm.log.txt).
+constexpr int kCkptStoreAux = 0;
 
 // ---- wta_h.hip --------------------------------------------
 // Prefetch depth (steps) of the forward pass (1 cost load per step) and the
