@@ -239,7 +239,7 @@ def load_traffic(workload, kernel="sgm_paths"):
 
 
 # rocprofv3 kernel names -> bench timer names (the PMC pass reports per kernel)
-PMC_KERNELS = {"sgm_paths_kernel": "sgm_paths", "wta_h_kernel": "wta_h",
+PMC_KERNELS = {"sgm_paths_kernel": "sgm_paths", "wta_h_kernel": "wta_h", "wta_hv_kernel": "wta_hv",
                "census_cost_kernel": "cost"}
 
 
@@ -427,7 +427,7 @@ def exchange_report(a, step, world, rank, dev, ctxs, last, n_units, ms_per_step,
             "map_bytes_per_unit": int(last[0].numel() * last.element_size())}
 
 
-def kernel_table(ctx, names=("census", "cost", "sgm_paths", "wta_h", "fuse_depth")):
+def kernel_table(ctx, names=("census", "cost", "sgm_paths", "wta_h", "wta_hv", "fuse_depth")):
     """Average hipEvent duration per kernel, pooled over one or several contexts
     (with --streams > 1 the launches overlap, so durations include contention)."""
     ctxs = ctx if isinstance(ctx, list) else [ctx]

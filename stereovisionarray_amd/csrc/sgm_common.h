@@ -31,9 +31,14 @@ struct PathGeom {
     int blk_h;    // blocks per horizontal direction (H lines)
     int blk_w;    // blocks per vertical / diagonal direction (W lines)
     size_t vol;   // bytes of one direction volume (W*H*D)
-    int ckpt;     // 1: horizontal lines store only segment checkpoints (below)
-    int ns;       // checkpoint segments per row, ceil(W / kSeg)
+    int ckpt;     // 1: horizontal lines store only segment checkpoints (below);
+                  // 2: vertical lines too (tile pipeline, wta_hv.hip)
+    int ns;       // checkpoint segments per row, ceil(W / 2^hsl)
     size_t ckvol; // bytes of one direction's checkpoint plane (H*ns*D)
+    int hsl;      // log2 of the horizontal checkpoint segment (columns)
+    int vsl;      // ckpt 2: log2 of the vertical checkpoint segment (rows)
+    int nsy;      // ckpt 2: vertical checkpoint segments per column, ceil(H / 2^vsl)
+    size_t ckvvol; // ckpt 2: bytes of one vertical checkpoint plane (nsy*W*D)
 };
 
 // Horizontal-line checkpoints.  With g.ckpt set, the two
@@ -250,9 +255,9 @@ template <int DPL> constexpr int pf_v() {
 
 
 // One path line over a materialised cost volume C.  CKPT
-// (horizontal lines only): store segment checkpoints to rCK instead of the
-// full L_r line to rL.
-template <int DPL, bool DIAG, int PF, bool CKPT = false>
+// 1 (horizontal lines) / 2 (vertical lines): store segment checkpoints to rCK
+// instead of the full L_r line to rL.
+template <int DPL, bool DIAG, int PF, int CKPT = 0>
 __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& g, int rx, int ry,
                                           int line, int k, rsrc_t rCK) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
@@ -324,14 +329,25 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
         for (int w = 0; w < NW; w++) cw[w] = ring[p].w[w];
         unsigned ow[NW];
         sgm_step<DPL>(cw, A, m, ow, P1, P2, edges);
-        if constexpr (CKPT) {
+        if constexpr (CKPT == 1) {
             // ts is the (wave-uniform) step index; x the pixel just computed
             const int x = rx > 0 ? ts : W - 1 - ts;
-            constexpr int SL = seg_log2<DPL>(), SEG = 1 << SL;
+            const int SL = g.hsl, SEG = 1 << SL;
             const bool hit = rx > 0 ? (((x + 1) & (SEG - 1)) == 0 && x + 1 < W)
                                     : ((x & (SEG - 1)) == 0 && x > 0);
             if (hit)   // default policy (tune::kCkptStoreAux): the WTA kernel reads these back soon
                 bstore<NW, tune::kCkptStoreAux>(rCK, ((unsigned)(y0 * g.ns + (x >> SL)) * (unsigned)D +
+                                         (unsigned)(k * DPL)), ow);
+        } else if constexpr (CKPT == 2) {
+            // vertical line x0: direction 2 (down) keeps the last row of every
+            // row segment but the column's last, direction 3 (up) the first row
+            // of every segment but the first; [nsy][W][D] per direction
+            const int y = ry > 0 ? ts : H - 1 - ts;
+            const int SL = g.vsl, SEG = 1 << SL;
+            const bool hit = ry > 0 ? (((y + 1) & (SEG - 1)) == 0 && y + 1 < H)
+                                    : ((y & (SEG - 1)) == 0 && y > 0);
+            if (hit)
+                bstore<NW, tune::kCkptStoreAux>(rCK, ((unsigned)((y >> SL) * W + x0) * (unsigned)D +
                                          (unsigned)(k * DPL)), ow);
         } else {
             bstore<NW>(rL, cc.off, ow);
@@ -385,6 +401,49 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
         if (t + p < steps) step(p, false, t + p);
 }
 
+
+// ---- shared by the final kernels (wta_h.hip, wta_hv.hip) ------------------
+
+template <int NW>
+__device__ __forceinline__ void unpack_add(const unsigned (&w)[NW], unsigned (&S)[2 * NW]) {
+#pragma unroll
+    for (int q = 0; q < NW; q++) {
+        unsigned a, b;
+        unpack4(w[q], a, b);
+        S[2 * q] += a;        // packed add: S <= 8 * 255 < 2^16 per half, no carry
+        S[2 * q + 1] += b;
+    }
+}
+
+// Path state from a u8 checkpoint: A = L(q) as packed pairs, m = min_k L(q).
+// Padded disparities (PAD) held L >= 255 in the path kernel, which the u8
+// checkpoint truncated; they restart at 255.  Every real disparity evolves
+// the same from 255 as from the true value: a padded neighbour enters only
+// as A + P1 >= 255 >= m + P2 (m <= 62), and never sets the row minimum.
+template <int DPL, bool PAD>
+__device__ __forceinline__ void state_from_words(const Words<DPL / 4>& w, unsigned (&A)[DPL / 2],
+                                                 unsigned& m, const unsigned (&padm)[DPL / 2]) {
+    constexpr int NW = DPL / 4, NP = DPL / 2;
+#pragma unroll
+    for (int q = 0; q < NW; q++) unpack4(w.w[q], A[2 * q], A[2 * q + 1]);
+    if constexpr (PAD) {
+#pragma unroll
+        for (int j = 0; j < NP; j++) A[j] |= padm[j] & 0x00ff00ffu;   // A < 256: OR = max
+    }
+    unsigned mm = 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+        const unsigned lo = A[j] & 0xffffu, hi = A[j] >> 16;
+        mm = mm < lo ? mm : lo;
+        mm = mm < hi ? mm : hi;
+    }
+    m = row_min_u32(mm);
+}
+template <int DPL, bool PAD>
+__device__ __forceinline__ void load_state(rsrc_t r, unsigned off, unsigned (&A)[DPL / 2],
+                                           unsigned& m, const unsigned (&padm)[DPL / 2]) {
+    state_from_words<DPL, PAD>(bload<DPL / 4>(r, off), A, m, padm);
+}
 
 }  // namespace sgm
 }  // namespace sva

@@ -31,6 +31,11 @@
 //      directions write [6][H][W][D] (direction r at slot r - 2); the two
 //      horizontal ones store only segment checkpoints, [2][H][ns][D], and
 //      wta_h.hip recomputes them per segment: 8 C reads + 6 L writes.
+//   2  the tile pipeline: only the four diagonal directions
+//      write volumes, [4][H][W][D] (direction r at slot r - 4); horizontal
+//      lines store checkpoints every 2^hsl columns, vertical lines every 2^vsl
+//      rows ([2][nsy][W][D]), and wta_hv.hip recomputes all four per tile:
+//      8 C reads + 4 L writes.
 #include "sgm_common.h"
 #include "sva_tuning.h"
 
@@ -46,6 +51,7 @@ template <int DPL>
 __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __restrict__ C,
                                                                uint8_t* __restrict__ L8,
                                                                uint8_t* __restrict__ CK,
+                                                               uint8_t* __restrict__ CKV,
                                                                PathGeom g) {
     // Horizontal directions (W steps per line, the longest) get the lowest
     // block ids and issue priority so they are never the tail.
@@ -74,16 +80,19 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
     int rx, ry;
     dir_of(r, rx, ry);
     const rsrc_t rC = make_rsrc(C, g.vol);
-    const int slot = g.ckpt ? r - 2 : r;
+    const int slot = g.ckpt == 2 ? r - 4 : g.ckpt ? r - 2 : r;
     if (r >= 4) {
         const rsrc_t rL = make_rsrc(L8 + (size_t)slot * g.vol, g.vol);
         path_line<DPL, true, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
+    } else if (r >= 2 && g.ckpt == 2) {
+        const rsrc_t rCK = make_rsrc(CKV + (size_t)(r - 2) * g.ckvvol, g.ckvvol);
+        path_line<DPL, false, pf_v<DPL>(), 2>(rC, rC, g, rx, ry, line, k, rCK);
     } else if (r >= 2) {
         const rsrc_t rL = make_rsrc(L8 + (size_t)slot * g.vol, g.vol);
         path_line<DPL, false, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
     } else if (g.ckpt) {
         const rsrc_t rCK = make_rsrc(CK + (size_t)r * g.ckvol, g.ckvol);
-        path_line<DPL, false, pf_h<DPL>(), true>(rC, rC, g, rx, ry, line, k, rCK);
+        path_line<DPL, false, pf_h<DPL>(), 1>(rC, rC, g, rx, ry, line, k, rCK);
     } else {
         const rsrc_t rL = make_rsrc(L8 + (size_t)r * g.vol, g.vol);
         path_line<DPL, false, pf_h<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
@@ -98,22 +107,46 @@ int sgm_seg_log2(int D) { return seg_log2_of(D); }
 
 int ckpt_segments(int W, int D) { return (W + (1 << seg_log2_of(D)) - 1) >> seg_log2_of(D); }
 
+TileGeom tile_geom(int W, int H, int D) {
+    TileGeom t;
+    t.seg_log2 = D <= 128 ? tune::kWtahvTileLog2 : tune::kWtahvTileLog2Wide;
+    const int seg = 1 << t.seg_log2;
+    t.ntx = (W + 15) >> 4;
+    t.nty = (H + seg - 1) >> t.seg_log2;
+    t.nsx = (W + seg - 1) >> t.seg_log2;
+    t.hck_bytes = 2 * (size_t)H * t.nsx * D;
+    t.vck_bytes = 2 * (size_t)t.nty * W * D;
+    return t;
+}
+
 hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
-                        uint8_t* L8, uint8_t* CK) {
+                        uint8_t* L8, uint8_t* CK, uint8_t* CKV) {
     DispatchTimer t(c, "sgm_paths");
     PathGeom g;
     g.W = W; g.H = H; g.D = D; g.P1 = P1; g.P2 = P2;
     g.blk_h = (H + LINES_PER_BLOCK - 1) / LINES_PER_BLOCK;
     g.blk_w = (W + LINES_PER_BLOCK - 1) / LINES_PER_BLOCK;
     g.vol = (size_t)W * H * D;
-    g.ckpt = CK != nullptr;
-    g.ns = ckpt_segments(W, D);
+    g.ckpt = CKV ? 2 : CK ? 1 : 0;
+    g.hsl = seg_log2_of(D);
+    g.vsl = 0;
+    g.nsy = 0;
+    g.ckvvol = 0;
+    if (CKV) {
+        if (!CK) return hipErrorInvalidValue;
+        const TileGeom tg = tile_geom(W, H, D);
+        g.hsl = tg.seg_log2;
+        g.vsl = tg.seg_log2;
+        g.nsy = tg.nty;
+        g.ckvvol = tg.vck_bytes / 2;
+    }
+    g.ns = (W + (1 << g.hsl) - 1) >> g.hsl;
     g.ckvol = (size_t)H * g.ns * D;
     if (g.vol >= (size_t)1 << 32) return hipErrorInvalidValue;  // 32-bit buffer offsets
     dim3 grid(2 * g.blk_h + 6 * g.blk_w);
 #define SVA_PATHS_LAUNCH(DPL_)                                                               \
     hipExtLaunchKernelGGL(sgm_paths_kernel<DPL_>, grid, dim3(PATH_BLOCK), 0, c.stream, t.start, \
-                          t.stop, 0, C, L8, CK, g);                                    \
+                          t.stop, 0, C, L8, CK, CKV, g);                                    \
     t.used = true
     switch (D) {
         case 64: SVA_PATHS_LAUNCH(4); break;

@@ -175,6 +175,21 @@ size_t ckpt_bytes(int W, int H, int D) { return 2 * (size_t)H * ckpt_segments(W,
 int paths_wta(Ctx* c, const uint8_t* C, int W, int H, const sva_sgm_params* p, int Dp,
               uint16_t* disp, float* sub) {
     const size_t nv = (size_t)W * H * (size_t)Dp;
+    if (wta_hv_supported(Dp)) {
+        // tile pipeline: four diagonal volumes + horizontal
+        // and vertical checkpoints, recomputed per tile by wta_hv
+        const TileGeom tg = tile_geom(W, H, Dp);
+        SVA_HIP(c, c->paths.ensure(nv * 4), "path workspace");
+        SVA_HIP(c, c->ckpt.ensure(tg.hck_bytes + tg.vck_bytes), "checkpoint workspace");
+        uint8_t* L4 = (uint8_t*)c->paths.ptr;
+        uint8_t* CK = (uint8_t*)c->ckpt.ptr;
+        uint8_t* CKV = CK + tg.hck_bytes;
+        SVA_HIP(c, launch_paths(*c, C, W, H, Dp, p->P1, p->P2, L4, CK, CKV), "paths launch");
+        SVA_HIP(c, launch_wta_hv(*c, C, L4, CK, CKV, W, H, Dp, p->P1, p->P2, p->dmin, disp, sub,
+                                 p->D),
+                "wta launch");
+        return SVA_OK;
+    }
     SVA_HIP(c, c->paths.ensure(nv * 6), "path workspace");
     SVA_HIP(c, c->ckpt.ensure(ckpt_bytes(W, H, Dp)), "checkpoint workspace");
     uint8_t* L6 = (uint8_t*)c->paths.ptr;
@@ -428,7 +443,12 @@ int sva_reserve(void* ctx, int W, int H, int D) {
     SVA_HIP(c, c->census_r.ensure(np * 8), "reserve");
     SVA_HIP(c, c->cost.ensure(nv), "reserve");
     SVA_HIP(c, c->paths.ensure(nv * 6), "reserve");
-    SVA_HIP(c, c->ckpt.ensure(ckpt_bytes(W, H, D)), "reserve");
+    size_t ck = ckpt_bytes(W, H, D);                  // stage API / wta_h route
+    if (wta_hv_supported(D)) {                        // the tile pipeline's frames
+        const TileGeom tg = tile_geom(W, H, D);
+        ck = std::max(ck, tg.hck_bytes + tg.vck_bytes);
+    }
+    SVA_HIP(c, c->ckpt.ensure(ck), "reserve");
     return SVA_OK;
 }
 

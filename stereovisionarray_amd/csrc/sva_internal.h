@@ -132,8 +132,21 @@ hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, in
 // sgm_paths.hip -- all 8 directions in one launch.  CK == nullptr: L8 =
 // [8][H][W][D] u8.  CK set (checkpoint mode): L8 = [6][H][W][D]
 // (directions 2..7) and CK = [2][H][ckpt_segments(W, D)][D] horizontal states.
+// CKV set as well (tile mode): L8 = [4][H][W][D] (directions
+// 4..7), CK = [2][H][nsx][D] and CKV = [2][nsy][W][D] (tile_geom below).
 hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
-                        uint8_t* L8, uint8_t* CK = nullptr);
+                        uint8_t* L8, uint8_t* CK = nullptr, uint8_t* CKV = nullptr);
+// Tile pipeline geometry: tiles of 16 columns x seg rows (seg = 2^seg_log2),
+// checkpoints every seg columns (horizontal lines) and every seg rows
+// (vertical lines).
+struct TileGeom {
+    int seg_log2;
+    int ntx, nty;             // tiles per row / per column (nty = vertical segments)
+    int nsx;                  // horizontal segments per row
+    size_t hck_bytes;         // [2][H][nsx][D]
+    size_t vck_bytes;         // [2][nty][W][D]
+};
+TileGeom tile_geom(int W, int H, int D);
 bool paths_supported(int D);
 // Native volume width of a frame with D disparities: 64, 128, 192 or 256
 // (the smallest >= D), 0 when D is outside 1..256.
@@ -147,6 +160,13 @@ int sgm_seg_log2(int D);
 hipError_t launch_wta_h(Ctx& c, const uint8_t* C, const uint8_t* L6, const uint8_t* CK, int W,
                         int H, int D, int P1, int P2, int dmin, uint16_t* disp, float* sub,
                         int dreal = 0);
+// wta_hv.hip -- the tile pipeline's final kernel: horizontal + vertical
+// recompute from the checkpoints of launch_paths(.., CK, CKV), sum with the
+// four diagonal volumes L4, WTA.
+bool wta_hv_supported(int D);
+hipError_t launch_wta_hv(Ctx& c, const uint8_t* C, const uint8_t* L4, const uint8_t* CK,
+                         const uint8_t* CKV, int W, int H, int D, int P1, int P2, int dmin,
+                         uint16_t* disp, float* sub, int dreal = 0);
 // wta.hip
 hipError_t launch_sum(Ctx& c, const uint8_t* L8, int W, int H, int D, uint16_t* S);
 hipError_t launch_wta_from_sum(Ctx& c, const uint16_t* S, int W, int H, int D, int dmin,

@@ -45,6 +45,20 @@ constexpr int kWtahPfFwdWide = 4, kWtahPfBwdWide = 4;
 // pass (0 = the whole segment); the others are re-read from global memory.
 constexpr int kWtahLdsPix = 0;
 
+// ---- wta_hv.hip -------------------------------------------
+// log2 of the tile rows and of the checkpoint segment (tiles are 16 x 2^this).
+constexpr int kWtahvTileLog2 = 3;
+constexpr int kWtahvTileLog2Wide = 3;      // D > 128
+// Prefetch depth (pixels) of the four diagonal-volume loads in the last pass.
+constexpr int kWtahvPfVol = 4;
+// Phase V's opposite recurrences one after the other (0) or interleaved (1).
+constexpr int kWtahvInterleaveV = 0;
+// Phase H's checkpoint and first volume loads issued before the barrier.
+constexpr int kWtahvEarlyLoads = 1;
+// Phase H's cost words loaded with phase V's at the start (1) or after phase
+// V's recurrences (0).
+constexpr int kWtahvRowCFirst = 1;
+
 // ---- census.hip / census_cost.hip / cost.hip ------------
 // Rows per workgroup of the multi-row census kernel.
 constexpr int kCensusRows = 16;

@@ -49,43 +49,6 @@ template <int DPL> constexpr int pf_bwd() { return DPL <= 8 ? tune::kWtahPfBwd :
 // default policy is 9 % faster (profiles/r02_v9/ab_wtah_pf.log).
 template <int DPL> constexpr int vol_aux() { return DPL <= 4 ? 0 : 2; }
 
-template <int NW>
-__device__ __forceinline__ void unpack_add(const unsigned (&w)[NW], unsigned (&S)[2 * NW]) {
-#pragma unroll
-    for (int q = 0; q < NW; q++) {
-        unsigned a, b;
-        unpack4(w[q], a, b);
-        S[2 * q] += a;        // packed add: S <= 8 * 255 < 2^16 per half, no carry
-        S[2 * q + 1] += b;
-    }
-}
-
-// Path state from a u8 checkpoint: A = L(q) as packed pairs, m = min_k L(q).
-// Padded disparities (PAD) held L >= 255 in the path kernel, which the u8
-// checkpoint truncated; they restart at 255.  Every real disparity evolves
-// the same from 255 as from the true value: a padded neighbour enters only
-// as A + P1 >= 255 >= m + P2 (m <= 62), and never sets the row minimum.
-template <int DPL, bool PAD>
-__device__ __forceinline__ void load_state(rsrc_t r, unsigned off, unsigned (&A)[DPL / 2],
-                                           unsigned& m, const unsigned (&padm)[DPL / 2]) {
-    constexpr int NW = DPL / 4, NP = DPL / 2;
-    const Words<NW> w = bload<NW>(r, off);
-#pragma unroll
-    for (int q = 0; q < NW; q++) unpack4(w.w[q], A[2 * q], A[2 * q + 1]);
-    if constexpr (PAD) {
-#pragma unroll
-        for (int j = 0; j < NP; j++) A[j] |= padm[j] & 0x00ff00ffu;   // A < 256: OR = max
-    }
-    unsigned mm = 0xffffffffu;
-#pragma unroll
-    for (int j = 0; j < NP; j++) {
-        const unsigned lo = A[j] & 0xffffu, hi = A[j] >> 16;
-        mm = mm < lo ? mm : lo;
-        mm = mm < hi ? mm : hi;
-    }
-    m = row_min_u32(mm);
-}
-
 template <int DPL, bool PAD>
 __global__ __launch_bounds__(HB) void wta_h_kernel(const uint8_t* __restrict__ C,
                                                    const uint8_t* __restrict__ L6,

@@ -1,0 +1,289 @@
+// wta_hv.hip -- the tile pipeline's final kernel (SURVEY.md
+// §8a rows A12-A13): horizontal AND vertical path recompute + path sum + WTA
+// (+ sub-pixel) per 16 x TY pixel tile.
+//
+// sgm_paths in tile mode (ckpt 2) leaves four u8 volumes (the diagonal
+// directions) and checkpoints every TY pixels: the horizontal lines' L state
+// at the last / first column of every TY-column segment, the vertical lines'
+// at the last / first row of every TY-row segment.  One 256-thread workgroup
+// owns one tile of 16 columns x TY rows, with the path kernel's lane layout
+// (lane k of a 16-lane DPP row owns disparities [k*DPL, k*DPL + DPL)):
+//   phase V  row-slot s runs column x0 + s: the downward recurrence over the
+//            tile's rows from the checkpoint above the tile, and the upward
+//            one from the checkpoint below it; V = L_2 + L_3 of every pixel
+//            goes to LDS (u16 pairs).
+//   phase H  row-slot s runs one TY-pixel row segment (16 / TY per tile row):
+//            left-to-right from the checkpoint left of it (L_0 kept in
+//            registers, u8-packed), then right-to-left from the one right of
+//            it; at each pixel S = L_1 + L_0 + V + the four diagonal volumes,
+//            and the first-minimum WTA (+ parabola) picks d*.
+// Every recurrence restarts from the exact state the path kernel had, so L,
+// S, d* and the sub-pixel value are bit-identical to the 8-volume route.
+//
+// Bytes per disparity: 1 C read (phase H re-reads the tile's cost words from
+// L2, where phase V just brought them) + 4 volume reads, and the path kernel
+// writes 4 volumes instead of 6: -4 B/disp against the wta_h route (§4.6).
+#include "sgm_common.h"
+#include "wta_common.h"
+#include "sva_tuning.h"
+
+namespace sva {
+namespace {
+
+using namespace sgm;
+
+constexpr int TB = 256;             // 16 slots of 16 lanes
+constexpr int TW = 16;              // tile columns
+
+struct WtaHvGeom {
+    int W, H, D, P1, P2, dmin;
+    int ntx, nty;     // tiles per row / per column
+    int nsx;          // horizontal checkpoint segments per row, ceil(W / TY)
+    int dreal;        // disparities of the caller (< D: padded frame)
+    unsigned vol;     // bytes of one [H][W][D] volume (< 2^32)
+    unsigned hck;     // bytes of one horizontal checkpoint plane [H][nsx][D]
+    unsigned vck;     // bytes of one vertical checkpoint plane [nty][W][D]
+};
+
+// Prefetch depth (pixels) of the diagonal volumes in the last pass.
+constexpr int kPfVol = tune::kWtahvPfVol;
+
+template <int DPL, int TYL, bool PAD>
+__global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ C,
+                                                    const uint8_t* __restrict__ L4,
+                                                    const uint8_t* __restrict__ CK,
+                                                    const uint8_t* __restrict__ CKV, WtaHvGeom g,
+                                                    uint16_t* __restrict__ disp,
+                                                    float* __restrict__ sub) {
+    constexpr int NW = DPL / 4, NP = DPL / 2;
+    constexpr int TY = 1 << TYL;        // tile rows = checkpoint segment (rows and columns)
+    constexpr int SPR = TW / TY;        // phase H: row segments per tile row
+    static_assert(TY <= TW && TW % TY == 0, "tile rows must divide 16");
+    const int tx = (int)(blockIdx.x % (unsigned)g.ntx);
+    const int ty = (int)(blockIdx.x / (unsigned)g.ntx);
+    const int slot = (int)(threadIdx.x >> 4);
+    const int k = (int)(threadIdx.x & 15);
+    const int W = g.W, H = g.H;
+    const unsigned uD = (unsigned)g.D, uW = (unsigned)W;
+    const unsigned P1 = (unsigned)g.P1, P2 = (unsigned)g.P2;
+    const int x0 = tx * TW, y0 = ty * TY;
+    const int nx = W - x0 < TW ? W - x0 : TW;       // tile columns inside the image (uniform)
+    const int ny = H - y0 < TY ? H - y0 : TY;       // tile rows inside the image (uniform)
+    const unsigned lane_d = (unsigned)(k * DPL);
+    const rsrc_t rC = make_rsrc(C, g.vol);
+    unsigned padm[NP];
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+        const int d = k * DPL + 2 * j;
+        padm[j] = PAD ? ((d >= g.dreal ? 0x0000ffffu : 0u) | (d + 1 >= g.dreal ? 0xffff0000u : 0u))
+                      : 0u;
+    }
+
+    // V = L_2 + L_3 per tile pixel, [pixel = r * TW + c][lane k][NP pairs]:
+    // each 16-lane row reads / writes 16 consecutive NP-dword chunks.
+    __shared__ unsigned vsum[TY * TW * 16 * NP];
+
+    // phase V: column x0 + slot; phase H: row hr, columns [hx, hx + TY)
+    const bool vcol = slot < nx;
+    const int hr = slot / SPR, hseg = slot % SPR;
+    const int hx = x0 + hseg * TY;                    // first column of the row segment
+    const int nh = W - hx < TY ? W - hx : TY;         // its pixels inside the image
+    const bool hrow = hr < ny && nh > 0;
+    const unsigned xv = (unsigned)(x0 + slot), yh = (unsigned)(y0 + hr);
+
+    // Both phases' cost words are loaded up front (tune::kWtahvRowCFirst): the
+    // tile's column slice for phase V and its row slice for phase H (the same
+    // bytes, L2-hot the second time).
+    Words<NW> cv[TY], ch[TY];
+#pragma unroll
+    for (int r = 0; r < TY; r++)
+        cv[r] = bload<NW>(rC, ((unsigned)(y0 + r) * uW + xv) * uD + lane_d);
+    auto load_row = [&]() {
+#pragma unroll
+        for (int j = 0; j < TY; j++)
+            ch[j] = bload<NW>(rC, (yh * uW + (unsigned)(hx + j)) * uD + lane_d);
+    };
+    if constexpr (tune::kWtahvRowCFirst != 0) load_row();
+
+    auto zero_state = [](unsigned (&A)[NP], unsigned& m) {
+#pragma unroll
+        for (int j = 0; j < NP; j++) A[j] = 0u;   // L(q) = 0, m = 0  =>  L = C
+        m = 0u;
+    };
+    unsigned Aa[NP], Ab[NP], ma, mb;
+    Edges ea, eb;
+    // ---- phase V: down (direction 2) and up (direction 3) ------------------
+    // tune::kWtahvInterleaveV: one after the other (0), or interleaved, step i
+    // of one next to step TY-1-i of the other (1: two independent dependency
+    // chains per wave).
+    if (vcol) {
+        if (ty > 0)
+            load_state<DPL, PAD>(make_rsrc(CKV, g.vck), ((unsigned)(ty - 1) * uW + xv) * uD + lane_d,
+                                 Aa, ma, padm);
+        else
+            zero_state(Aa, ma);
+        if (y0 + TY < H)
+            load_state<DPL, PAD>(make_rsrc(CKV + g.vck, g.vck),
+                                 ((unsigned)(ty + 1) * uW + xv) * uD + lane_d, Ab, mb, padm);
+        else
+            zero_state(Ab, mb);
+        auto put_v = [&](int r, const unsigned (&ld)[NW], const unsigned (&lu)[NW]) {
+            unsigned V[NP];
+#pragma unroll
+            for (int q = 0; q < NW; q++) unpack4(ld[q], V[2 * q], V[2 * q + 1]);
+            unpack_add<NW>(lu, V);                          // L_2 + L_3 (<= 510)
+            unsigned* dst = &vsum[((r * TW + slot) * 16 + k) * NP];
+#pragma unroll
+            for (int p = 0; p < NP; p++) dst[p] = V[p];
+        };
+        unsigned LD[TY][NW];
+        if constexpr (tune::kWtahvInterleaveV != 0) {
+            unsigned LU[TY][NW];
+            for_seq<TY>([&](auto I) {
+                constexpr int i = decltype(I)::value, ru = TY - 1 - i;
+                if (i < ny) sgm_step<DPL>(cv[i].w, Aa, ma, LD[i], P1, P2, ea);
+                if (ru < ny) sgm_step<DPL>(cv[ru].w, Ab, mb, LU[ru], P1, P2, eb);
+            });
+            for_seq<TY>([&](auto R) {
+                constexpr int r = decltype(R)::value;
+                if (r < ny) put_v(r, LD[r], LU[r]);
+            });
+        } else {
+            for_seq<TY>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                if (i < ny) sgm_step<DPL>(cv[i].w, Aa, ma, LD[i], P1, P2, ea);
+            });
+            for_seq<TY>([&](auto Q) {
+                constexpr int r = TY - 1 - decltype(Q)::value;
+                if (r < ny) {
+                    unsigned lu[NW];
+                    sgm_step<DPL>(cv[r].w, Ab, mb, lu, P1, P2, eb);
+                    put_v(r, LD[r], lu);
+                }
+            });
+        }
+    }
+    if constexpr (tune::kWtahvRowCFirst == 0) load_row();
+    // phase H's first global loads (checkpoints, diagonal volumes) go out
+    // before the barrier (tune::kWtahvEarlyLoads)
+    const int hs = hx >> TYL;                          // the row segment's index
+    const unsigned ckrow = yh * (unsigned)g.nsx;
+    Words<NW> ckw[2];
+    rsrc_t rV[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) rV[r] = make_rsrc(L4 + (size_t)r * g.vol, g.vol);
+    Words<NW> rv[kPfVol][4];
+    auto issue = [&](int s, int j) {
+        const unsigned off = (yh * uW + (unsigned)(hx + j)) * uD + lane_d;
+#pragma unroll
+        for (int r = 0; r < 4; r++) rv[s][r] = bload<NW, 2>(rV[r], off);   // last use: nt
+    };
+    auto issue_first = [&]() {
+        // (words outside the image are never used: the first / last segment
+        // starts from zero state)
+        ckw[0] = bload<NW>(make_rsrc(CK, g.hck), (ckrow + (unsigned)(hs - 1)) * uD + lane_d);
+        ckw[1] = bload<NW>(make_rsrc(CK + g.hck, g.hck), (ckrow + (unsigned)(hs + 1)) * uD + lane_d);
+#pragma unroll
+        for (int q = 0; q < kPfVol && q < TY; q++) issue(q, TY - 1 - q);
+    };
+    if constexpr (tune::kWtahvEarlyLoads != 0) {
+        if (hrow) issue_first();
+    }
+    __syncthreads();
+
+    // ---- phase H: left-to-right (direction 0), then right-to-left (1) with
+    // the sum and the WTA per pixel
+    if (!hrow) return;                                 // whole 16-lane row leaves together
+    if constexpr (tune::kWtahvEarlyLoads == 0) issue_first();
+    if (hs > 0) state_from_words<DPL, PAD>(ckw[0], Aa, ma, padm);
+    else zero_state(Aa, ma);
+    unsigned LF[TY][NW];
+    for_seq<TY>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        if (i < nh) sgm_step<DPL>(ch[i].w, Aa, ma, LF[i], P1, P2, ea);
+    });
+    if (hx + TY < W) state_from_words<DPL, PAD>(ckw[1], Aa, ma, padm);
+    else zero_state(Aa, ma);
+    unsigned dres = 0u, sm = 0u, s0 = 0u;
+    const bool want_sub = sub != nullptr;
+    for_seq<TY>([&](auto Q) {
+        constexpr int q = decltype(Q)::value, j = TY - 1 - q, s = q % kPfVol;
+        if (j < nh) {
+            unsigned ow[NW];
+            sgm_step<DPL>(ch[j].w, Aa, ma, ow, P1, P2, ea);
+            const unsigned* vs = &vsum[((hr * TW + hseg * TY + j) * 16 + k) * NP];
+            unsigned S[NP];
+#pragma unroll
+            for (int p = 0; p < NP; p++) S[p] = vs[p] + Aa[p];   // V + L_1
+            unpack_add<NW>(LF[j], S);                             // + L_0
+#pragma unroll
+            for (int r = 0; r < 4; r++) unpack_add<NW>(rv[s][r].w, S);
+            if constexpr (PAD) {
+#pragma unroll
+                for (int p = 0; p < NP; p++) S[p] |= padm[p];
+            }
+            unsigned spm, sb;
+            const int ds = wta_pick_raw<DPL>(S, k, want_sub, &spm, &sb);
+            if (k == j) {
+                dres = (unsigned)ds;
+                sm = spm;
+                s0 = sb;
+            }
+        }
+        if constexpr (q + kPfVol < TY) {
+            __builtin_amdgcn_sched_barrier(0);
+            issue(s, TY - 1 - (q + kPfVol));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    });
+    if (k < nh) {
+        const size_t at = (size_t)yh * (size_t)W + (size_t)(hx + k);
+        disp[at] = (uint16_t)(g.dmin + (int)dres);
+        if (want_sub) sub[at] = subpixel(g.dmin, (int)dres, g.dreal, sm & 0xffffu, s0, sm >> 16);
+    }
+}
+
+}  // namespace
+
+bool wta_hv_supported(int D) { return D == 64 || D == 128 || D == 192 || D == 256; }
+
+hipError_t launch_wta_hv(Ctx& c, const uint8_t* C, const uint8_t* L4, const uint8_t* CK,
+                         const uint8_t* CKV, int W, int H, int D, int P1, int P2, int dmin,
+                         uint16_t* disp, float* sub, int dreal) {
+    ScopedKernelTimer t(c, "wta_hv");
+    if (!wta_hv_supported(D)) return hipErrorInvalidValue;
+    const TileGeom tg = tile_geom(W, H, D);
+    WtaHvGeom g;
+    g.W = W; g.H = H; g.D = D; g.P1 = P1; g.P2 = P2; g.dmin = dmin;
+    g.dreal = dreal > 0 && dreal < D ? dreal : D;
+    g.ntx = tg.ntx;
+    g.nty = tg.nty;
+    g.nsx = tg.nsx;
+    const size_t vol = (size_t)W * H * D;
+    if (vol >= (size_t)1 << 32) return hipErrorInvalidValue;
+    g.vol = (unsigned)vol;
+    g.hck = (unsigned)(tg.hck_bytes / 2);
+    g.vck = (unsigned)(tg.vck_bytes / 2);
+    const bool pad = g.dreal < D;
+    const dim3 grid((unsigned)(g.ntx * g.nty));
+#define SVA_WTAHV(DPL_, TYL_)                                                                  \
+    if (pad)                                                                                   \
+        hipLaunchKernelGGL((wta_hv_kernel<DPL_, TYL_, true>), grid, dim3(TB), 0, c.stream, C,  \
+                           L4, CK, CKV, g, disp, sub);                                         \
+    else                                                                                       \
+        hipLaunchKernelGGL((wta_hv_kernel<DPL_, TYL_, false>), grid, dim3(TB), 0, c.stream, C, \
+                           L4, CK, CKV, g, disp, sub)
+    constexpr int TYL = tune::kWtahvTileLog2, TYLW = tune::kWtahvTileLog2Wide;
+    if (tg.seg_log2 != (D <= 128 ? TYL : TYLW)) return hipErrorInvalidValue;
+    switch (D) {
+        case 64: SVA_WTAHV(4, TYL); break;
+        case 128: SVA_WTAHV(8, TYL); break;
+        case 192: SVA_WTAHV(12, TYLW); break;
+        case 256: SVA_WTAHV(16, TYLW); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef SVA_WTAHV
+    return hipGetLastError();
+}
+
+}  // namespace sva

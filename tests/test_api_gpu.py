@@ -106,10 +106,10 @@ def test_reserve_timing_and_errors(ctx, sva):
     ctx.disparity_sgm(L, R, sva.default_params(D=128))
     ctx.disparity_sgm(L, R, sva.default_params(D=128))
     ctx.set_timing(False)
-    for name in ("cost", "sgm_paths", "wta_h"):      # the checkpoint-mode frame pipeline
+    for name in ("cost", "sgm_paths", "wta_hv"):     # the tile pipeline
         ms, n = ctx.kernel_time(name)
         assert n == 2 and ms > 0.0, name
-    assert ctx.kernel_time("wta") == (0.0, 0)
+    assert ctx.kernel_time("wta") == (0.0, 0) and ctx.kernel_time("wta_h") == (0.0, 0)
     # 1-D steps without the L/R check, D >= 128: census and cost are one kernel ("cost")
     assert ctx.kernel_time("census") == (0.0, 0)
     # AUTO (the default) and COST_VOLUME are the same route, D = 256 included
@@ -120,7 +120,7 @@ def test_reserve_timing_and_errors(ctx, sva):
         ctx.set_timing(True)
         ctx.disparity_sgm(L2, R2, sva.default_params(D=256))
         ctx.set_timing(False)
-        assert ctx.kernel_time("cost")[1] == 1 and ctx.kernel_time("wta_h")[1] == 1
+        assert ctx.kernel_time("cost")[1] == 1 and ctx.kernel_time("wta_hv")[1] == 1
     # the census-fused path kernel was removed in ABI v4
     with pytest.raises(sva.SvaError) as e:
         ctx.set_path_kernel(sva.SVA_PATH_KERNEL_FUSED)
@@ -136,7 +136,7 @@ def test_reserve_timing_and_errors(ctx, sva):
     ctx.disparity_sgm(L2, R2, sva.default_params(D=256))
     ctx.set_timing(sva.SVA_TIMING_OFF)
     assert ctx.kernel_time("sgm_paths")[1] == 2
-    for name in ("census", "cost", "wta", "wta_h"):
+    for name in ("census", "cost", "wta", "wta_h", "wta_hv"):
         assert ctx.kernel_time(name) == (0.0, 0), name
     with pytest.raises(sva.SvaError) as e:
         ctx.set_timing(3)

@@ -11,11 +11,13 @@ from stereovisionarray_amd import synth
 pytestmark = pytest.mark.gpu
 
 SIZES = [(1, 1), (2, 3), (9, 7), (8, 6), (17, 5), (5, 40), (63, 33), (65, 31), (129, 3),
-         (1, 70), (70, 1)]
+         (1, 70), (70, 1),
+         # around the tile pipeline's 16 x 8 tiles and 8-pixel checkpoint segments
+         (16, 8), (15, 9), (31, 17), (48, 24), (23, 16), (8, 1), (1, 8)]
 
 
 @pytest.mark.parametrize("W,H", SIZES)
-@pytest.mark.parametrize("D", [64, 256])
+@pytest.mark.parametrize("D", [64, 128, 192, 256])
 def test_tiny_and_ragged(ctx, sva, oracle, W, H, D):
     L = synth.texture(H, W, W * 7 + H)
     R = synth.texture(H, W, W * 7 + H + 1)
