@@ -33,11 +33,9 @@ struct PathGeom {
     size_t vol;   // bytes of one direction volume (W*H*D)
     int ckpt;     // 1: horizontal lines store only segment checkpoints (below);
                   // 2: vertical lines too (tile pipeline, wta_hv.hip)
-    int ns;       // checkpoint segments per row, ceil(W / 2^hsl)
+    int ns;       // checkpoint segments per row, ceil(W / seg)
     size_t ckvol; // bytes of one direction's checkpoint plane (H*ns*D)
-    int hsl;      // log2 of the horizontal checkpoint segment (columns)
-    int vsl;      // ckpt 2: log2 of the vertical checkpoint segment (rows)
-    int nsy;      // ckpt 2: vertical checkpoint segments per column, ceil(H / 2^vsl)
+    int nsy;      // ckpt 2: vertical checkpoint segments per column, ceil(H / seg)
     size_t ckvvol; // ckpt 2: bytes of one vertical checkpoint plane (nsy*W*D)
 };
 
@@ -255,9 +253,11 @@ template <int DPL> constexpr int pf_v() {
 
 
 // One path line over a materialised cost volume C.  CKPT
-// 1 (horizontal lines) / 2 (vertical lines): store segment checkpoints to rCK
-// instead of the full L_r line to rL.
-template <int DPL, bool DIAG, int PF, int CKPT = 0>
+// 1 (horizontal lines) / 2 (vertical lines): store checkpoints every 2^SL
+// pixels to rCK instead of the full L_r line to rL (SL is a template
+// parameter: a runtime segment test cost the latency-bound lines of small
+// frames 20 %).
+template <int DPL, bool DIAG, int PF, int CKPT = 0, int SL = 0>
 __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& g, int rx, int ry,
                                           int line, int k, rsrc_t rCK) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
@@ -332,7 +332,7 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
         if constexpr (CKPT == 1) {
             // ts is the (wave-uniform) step index; x the pixel just computed
             const int x = rx > 0 ? ts : W - 1 - ts;
-            const int SL = g.hsl, SEG = 1 << SL;
+            constexpr int SEG = 1 << SL;
             const bool hit = rx > 0 ? (((x + 1) & (SEG - 1)) == 0 && x + 1 < W)
                                     : ((x & (SEG - 1)) == 0 && x > 0);
             if (hit)   // default policy (tune::kCkptStoreAux): the WTA kernel reads these back soon
@@ -343,7 +343,7 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
             // row segment but the column's last, direction 3 (up) the first row
             // of every segment but the first; [nsy][W][D] per direction
             const int y = ry > 0 ? ts : H - 1 - ts;
-            const int SL = g.vsl, SEG = 1 << SL;
+            constexpr int SEG = 1 << SL;
             const bool hit = ry > 0 ? (((y + 1) & (SEG - 1)) == 0 && y + 1 < H)
                                     : ((y & (SEG - 1)) == 0 && y > 0);
             if (hit)

@@ -33,9 +33,9 @@
 //      wta_h.hip recomputes them per segment: 8 C reads + 6 L writes.
 //   2  the tile pipeline: only the four diagonal directions
 //      write volumes, [4][H][W][D] (direction r at slot r - 4); horizontal
-//      lines store checkpoints every 2^hsl columns, vertical lines every 2^vsl
-//      rows ([2][nsy][W][D]), and wta_hv.hip recomputes all four per tile:
-//      8 C reads + 4 L writes.
+//      lines store checkpoints every seg columns, vertical lines every seg
+//      rows ([2][nsy][W][D]; seg = 2^tile_geom().seg_log2), and wta_hv.hip
+//      recomputes all four per tile: 8 C reads + 4 L writes.
 #include "sgm_common.h"
 #include "sva_tuning.h"
 
@@ -81,18 +81,24 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
     dir_of(r, rx, ry);
     const rsrc_t rC = make_rsrc(C, g.vol);
     const int slot = g.ckpt == 2 ? r - 4 : g.ckpt ? r - 2 : r;
+    // checkpoint segments: the §4.6 route's, or the tile pipeline's (§4.9)
+    constexpr int SL1 = seg_log2<DPL>();
+    constexpr int SL2 = DPL <= 8 ? tune::kWtahvTileLog2 : tune::kWtahvTileLog2Wide;
     if (r >= 4) {
         const rsrc_t rL = make_rsrc(L8 + (size_t)slot * g.vol, g.vol);
         path_line<DPL, true, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
     } else if (r >= 2 && g.ckpt == 2) {
         const rsrc_t rCK = make_rsrc(CKV + (size_t)(r - 2) * g.ckvvol, g.ckvvol);
-        path_line<DPL, false, pf_v<DPL>(), 2>(rC, rC, g, rx, ry, line, k, rCK);
+        path_line<DPL, false, pf_v<DPL>(), 2, SL2>(rC, rC, g, rx, ry, line, k, rCK);
     } else if (r >= 2) {
         const rsrc_t rL = make_rsrc(L8 + (size_t)slot * g.vol, g.vol);
         path_line<DPL, false, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
     } else if (g.ckpt) {
         const rsrc_t rCK = make_rsrc(CK + (size_t)r * g.ckvol, g.ckvol);
-        path_line<DPL, false, pf_h<DPL>(), 1>(rC, rC, g, rx, ry, line, k, rCK);
+        if (g.ckpt == 2)
+            path_line<DPL, false, pf_h<DPL>(), 1, SL2>(rC, rC, g, rx, ry, line, k, rCK);
+        else
+            path_line<DPL, false, pf_h<DPL>(), 1, SL1>(rC, rC, g, rx, ry, line, k, rCK);
     } else {
         const rsrc_t rL = make_rsrc(L8 + (size_t)r * g.vol, g.vol);
         path_line<DPL, false, pf_h<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
@@ -128,19 +134,17 @@ hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, i
     g.blk_w = (W + LINES_PER_BLOCK - 1) / LINES_PER_BLOCK;
     g.vol = (size_t)W * H * D;
     g.ckpt = CKV ? 2 : CK ? 1 : 0;
-    g.hsl = seg_log2_of(D);
-    g.vsl = 0;
+    int hsl = seg_log2_of(D);            // the kernel's SL1 / SL2 for this D
     g.nsy = 0;
     g.ckvvol = 0;
     if (CKV) {
         if (!CK) return hipErrorInvalidValue;
         const TileGeom tg = tile_geom(W, H, D);
-        g.hsl = tg.seg_log2;
-        g.vsl = tg.seg_log2;
+        hsl = tg.seg_log2;
         g.nsy = tg.nty;
         g.ckvvol = tg.vck_bytes / 2;
     }
-    g.ns = (W + (1 << g.hsl) - 1) >> g.hsl;
+    g.ns = (W + (1 << hsl) - 1) >> hsl;
     g.ckvol = (size_t)H * g.ns * D;
     if (g.vol >= (size_t)1 << 32) return hipErrorInvalidValue;  // 32-bit buffer offsets
     dim3 grid(2 * g.blk_h + 6 * g.blk_w);

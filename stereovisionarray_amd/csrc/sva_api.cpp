@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "sva_internal.h"
+#include "sva_tuning.h"
 
 using namespace sva;
 
@@ -166,6 +167,12 @@ int check_sgm(Ctx* c, const sva_sgm_params* p, int W, int H, bool native = false
     return SVA_OK;
 }
 
+// The frame route: the tile pipeline (§4.9) unless a small D = 64 frame, where
+// the §4.6 route is faster (tune::kTileMinPixelsD64).
+bool use_tiles(int W, int H, int Dp) {
+    return wta_hv_supported(Dp) && (Dp > 64 || (long)W * H >= tune::kTileMinPixelsD64);
+}
+
 size_t ckpt_bytes(int W, int H, int D) { return 2 * (size_t)H * ckpt_segments(W, D) * (size_t)D; }
 
 // Paths + WTA of the cost-volume frame pipeline: sgm_paths
@@ -175,7 +182,7 @@ size_t ckpt_bytes(int W, int H, int D) { return 2 * (size_t)H * ckpt_segments(W,
 int paths_wta(Ctx* c, const uint8_t* C, int W, int H, const sva_sgm_params* p, int Dp,
               uint16_t* disp, float* sub) {
     const size_t nv = (size_t)W * H * (size_t)Dp;
-    if (wta_hv_supported(Dp)) {
+    if (use_tiles(W, H, Dp)) {
         // tile pipeline: four diagonal volumes + horizontal
         // and vertical checkpoints, recomputed per tile by wta_hv
         const TileGeom tg = tile_geom(W, H, Dp);
@@ -444,7 +451,7 @@ int sva_reserve(void* ctx, int W, int H, int D) {
     SVA_HIP(c, c->cost.ensure(nv), "reserve");
     SVA_HIP(c, c->paths.ensure(nv * 6), "reserve");
     size_t ck = ckpt_bytes(W, H, D);                  // stage API / wta_h route
-    if (wta_hv_supported(D)) {                        // the tile pipeline's frames
+    if (use_tiles(W, H, D)) {                         // the tile pipeline's frames
         const TileGeom tg = tile_geom(W, H, D);
         ck = std::max(ck, tg.hck_bytes + tg.vck_bytes);
     }

@@ -153,7 +153,8 @@ def main():
                 torch.cuda.synchronize()
                 outs.append((disp.cpu().numpy().tobytes(),
                              subm.cpu().numpy().tobytes() if a.sub else b""))
-            assert all(o == outs[0] for o in outs), "variants disagree on the disparity map"
+            if not os.environ.get("AB_NOCHECK"):     # ablation builds compute other values
+                assert all(o == outs[0] for o in outs), "variants disagree on the disparity map"
         if a.entry == "paths" and it == 0:
             # every variant must produce the same volumes
             outs = []
