@@ -16,7 +16,6 @@
 #include <vector>
 
 #include "sva_internal.h"
-#include "sva_tuning.h"
 
 using namespace sva;
 
@@ -167,10 +166,11 @@ int check_sgm(Ctx* c, const sva_sgm_params* p, int W, int H, bool native = false
     return SVA_OK;
 }
 
-// The frame route: the tile pipeline (§4.9) unless a small D = 64 frame, where
-// the §4.6 route is faster (tune::kTileMinPixelsD64).
+// The frame route: the tile pipeline (§4.9) at every native D; it was the
+// faster route at every frame size measured, 640x480 D=64 included.
 bool use_tiles(int W, int H, int Dp) {
-    return wta_hv_supported(Dp) && (Dp > 64 || (long)W * H >= tune::kTileMinPixelsD64);
+    (void)W; (void)H;
+    return wta_hv_supported(Dp);
 }
 
 size_t ckpt_bytes(int W, int H, int D) { return 2 * (size_t)H * ckpt_segments(W, D) * (size_t)D; }

@@ -46,12 +46,6 @@ constexpr int kWtahPfFwdWide = 4, kWtahPfBwdWide = 4;
 constexpr int kWtahLdsPix = 0;
 
 // ---- wta_hv.hip -------------------------------------------
-// Frames at D = 64 below this many pixels keep the §4.6 route (wta_h): their
-// volumes are too small for the saved bytes to pay for the recompute.  Frame
-// ms, §4.6 -> tiles (profiles/r03_v7/ab_route_sizes.log.txt): 640x480 0.136 ->
-// 0.147, 960x540 0.179 -> 0.198, 1280x720 0.291 -> 0.295, 1920x1080 0.586 ->
-// 0.541; at D >= 128 the tiles win from 640x480 up (D=128 0.198 -> 0.185).
-constexpr long kTileMinPixelsD64 = 1500000;
 // log2 of the tile rows and of the checkpoint segment (tiles are 16 x 2^this).
 constexpr int kWtahvTileLog2 = 3;
 constexpr int kWtahvTileLog2Wide = 3;      // D > 128
