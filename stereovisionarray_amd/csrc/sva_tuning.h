@@ -58,6 +58,12 @@ constexpr int kWtahvEarlyLoads = 1;
 // Phase H's cost words loaded with phase V's at the start (1) or after phase
 // V's recurrences (0).
 constexpr int kWtahvRowCFirst = 1;
+// Phase V's L_2 and phase H's L_0 kept per pixel as the step's u16 pairs (1:
+// V and S need only packed adds) or u8-packed (0: two v_perm per word to
+// re-expand, half the registers).  Above D = 128 the u16 copy costs a wave
+// per SIMD (D=192: 157 -> 169 VGPRs).
+constexpr int kWtahvKeepU16 = 1;
+constexpr int kWtahvKeepU16Wide = 0;
 
 // ---- census.hip / census_cost.hip / cost.hip ------------
 // Rows per workgroup of the multi-row census kernel.

@@ -57,6 +57,7 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
                                                     float* __restrict__ sub) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
     constexpr int TY = 1 << TYL;        // tile rows = checkpoint segment (rows and columns)
+    constexpr bool KEEP16 = DPL <= 8 ? tune::kWtahvKeepU16 != 0 : tune::kWtahvKeepU16Wide != 0;
     constexpr int SPR = TW / TY;        // phase H: row segments per tile row
     static_assert(TY <= TW && TW % TY == 0, "tile rows must divide 16");
     const int tx = (int)(blockIdx.x % (unsigned)g.ntx);
@@ -127,38 +128,62 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
                                  ((unsigned)(ty + 1) * uW + xv) * uD + lane_d, Ab, mb, padm);
         else
             zero_state(Ab, mb);
-        auto put_v = [&](int r, const unsigned (&ld)[NW], const unsigned (&lu)[NW]) {
-            unsigned V[NP];
+        // The down pass keeps each pixel's L_2 (KEEP16, tune::kWtahvKeepU16: as the
+        // step's u16 pairs, so V = L_2 + L_3 is NP packed adds; else u8-packed,
+        // re-expanded here with two v_perm per word).
+        constexpr int NK = KEEP16 ? NP : NW;
+        auto keep = [&](unsigned (&dst)[NK], const unsigned (&A)[NP], const unsigned (&ow)[NW]) {
 #pragma unroll
-            for (int q = 0; q < NW; q++) unpack4(ld[q], V[2 * q], V[2 * q + 1]);
-            unpack_add<NW>(lu, V);                          // L_2 + L_3 (<= 510)
+            for (int q = 0; q < NK; q++) dst[q] = KEEP16 ? A[q] : ow[q];
+        };
+        auto put_v = [&](int r, const unsigned (&ld)[NK], const unsigned (&Au)[NP],
+                         const unsigned (&lu)[NW]) {
+            unsigned V[NP];
+            if constexpr (KEEP16) {
+#pragma unroll
+                for (int p = 0; p < NP; p++) V[p] = ld[p] + Au[p];   // L_2 + L_3 (<= 510 per half)
+            } else {
+#pragma unroll
+                for (int q = 0; q < NW; q++) unpack4(ld[q], V[2 * q], V[2 * q + 1]);
+                unpack_add<NW>(lu, V);
+            }
             unsigned* dst = &vsum[((r * TW + slot) * 16 + k) * NP];
 #pragma unroll
             for (int p = 0; p < NP; p++) dst[p] = V[p];
         };
-        unsigned LD[TY][NW];
+        unsigned LD[TY][NK];
         if constexpr (tune::kWtahvInterleaveV != 0) {
-            unsigned LU[TY][NW];
+            unsigned LU[TY][NK];
             for_seq<TY>([&](auto I) {
                 constexpr int i = decltype(I)::value, ru = TY - 1 - i;
-                if (i < ny) sgm_step<DPL>(cv[i].w, Aa, ma, LD[i], P1, P2, ea);
-                if (ru < ny) sgm_step<DPL>(cv[ru].w, Ab, mb, LU[ru], P1, P2, eb);
+                unsigned ow[NW];
+                if (i < ny) { sgm_step<DPL>(cv[i].w, Aa, ma, ow, P1, P2, ea); keep(LD[i], Aa, ow); }
+                if (ru < ny) { sgm_step<DPL>(cv[ru].w, Ab, mb, ow, P1, P2, eb); keep(LU[ru], Ab, ow); }
             });
             for_seq<TY>([&](auto R) {
                 constexpr int r = decltype(R)::value;
-                if (r < ny) put_v(r, LD[r], LU[r]);
+                if (r < ny) {
+                    if constexpr (KEEP16) {
+                        const unsigned none[NW] = {};
+                        put_v(r, LD[r], LU[r], none);
+                    } else {
+                        unsigned V[NP] = {};
+                        put_v(r, LD[r], V, LU[r]);
+                    }
+                }
             });
         } else {
             for_seq<TY>([&](auto I) {
                 constexpr int i = decltype(I)::value;
-                if (i < ny) sgm_step<DPL>(cv[i].w, Aa, ma, LD[i], P1, P2, ea);
+                unsigned ow[NW];
+                if (i < ny) { sgm_step<DPL>(cv[i].w, Aa, ma, ow, P1, P2, ea); keep(LD[i], Aa, ow); }
             });
             for_seq<TY>([&](auto Q) {
                 constexpr int r = TY - 1 - decltype(Q)::value;
                 if (r < ny) {
                     unsigned lu[NW];
                     sgm_step<DPL>(cv[r].w, Ab, mb, lu, P1, P2, eb);
-                    put_v(r, LD[r], lu);
+                    put_v(r, LD[r], Ab, lu);
                 }
             });
         }
@@ -197,10 +222,17 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
     if constexpr (tune::kWtahvEarlyLoads == 0) issue_first();
     if (hs > 0) state_from_words<DPL, PAD>(ckw[0], Aa, ma, padm);
     else zero_state(Aa, ma);
-    unsigned LF[TY][NW];
+    // L_0 of the segment's pixels, kept like phase V's L_2 (KEEP16)
+    constexpr int NKH = KEEP16 ? NP : NW;
+    unsigned LF[TY][NKH];
     for_seq<TY>([&](auto I) {
         constexpr int i = decltype(I)::value;
-        if (i < nh) sgm_step<DPL>(ch[i].w, Aa, ma, LF[i], P1, P2, ea);
+        unsigned ow[NW];
+        if (i < nh) {
+            sgm_step<DPL>(ch[i].w, Aa, ma, ow, P1, P2, ea);
+#pragma unroll
+            for (int q = 0; q < NKH; q++) LF[i][q] = KEEP16 ? Aa[q] : ow[q];
+        }
     });
     if (hx + TY < W) state_from_words<DPL, PAD>(ckw[1], Aa, ma, padm);
     else zero_state(Aa, ma);
@@ -215,7 +247,12 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
             unsigned S[NP];
 #pragma unroll
             for (int p = 0; p < NP; p++) S[p] = vs[p] + Aa[p];   // V + L_1
-            unpack_add<NW>(LF[j], S);                             // + L_0
+            if constexpr (KEEP16) {
+#pragma unroll
+                for (int p = 0; p < NP; p++) S[p] += LF[j][p];     // + L_0
+            } else {
+                unpack_add<NW>(LF[j], S);
+            }
 #pragma unroll
             for (int r = 0; r < 4; r++) unpack_add<NW>(rv[s][r].w, S);
             if constexpr (PAD) {

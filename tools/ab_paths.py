@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--dir", type=int, default=-1)
     ap.add_argument("--sub", action="store_true", help="wta_h / sgm entries: also write the f32 sub-pixel map")
     ap.add_argument("--dmin", type=int, default=0)
+    ap.add_argument("--kernels", action="store_true",
+                    help="also report each variant's per-kernel hipEvent averages (timing mode 1 "
+                         "on every handle; the event packets slow every variant alike)")
     ap.add_argument("--entry", default="paths",
                     choices=["paths", "sgm", "cost", "census", "census_cost", "ckpt", "wta_h"])
     a = ap.parse_args()
@@ -56,6 +59,8 @@ def main():
         h = ct.c_void_p()
         assert lib.sva_create(0, ct.byref(h)) == 0
         assert lib.sva_set_stream(h, ct.c_void_p(s.cuda_stream)) == 0
+        lib.sva_kernel_time.argtypes = [ct.c_void_p, ct.c_char_p, ct.POINTER(ct.c_double),
+                                        ct.POINTER(ct.c_int64)]
         handles.append((os.path.basename(path), lib, h))
     # a real cost volume: run the full pipeline once with the first library
     name0, lib0, h0 = handles[0]
@@ -79,6 +84,10 @@ def main():
     times = {n: [] for n, _, _ in handles}
     ref = None
     for it in range(a.iters + 2):
+        if a.kernels and it == 2:            # kernel timing over the measured iterations only
+            for n, lib, h in handles:
+                lib.sva_set_timing(h, 1)
+                lib.sva_reset_timing(h)
         for n, lib, h in handles:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
@@ -166,6 +175,15 @@ def main():
             assert len(set(outs)) == 1, outs
     res = {n: {"median_ms": round(statistics.median(v), 4), "min_ms": round(min(v), 4)}
            for n, v in times.items()}
+    if a.kernels:
+        for n, lib, h in handles:
+            ks = {}
+            for k in ("cost", "census", "sgm_paths", "wta_h", "wta_hv"):
+                tot, cnt = ct.c_double(0), ct.c_int64(0)
+                lib.sva_kernel_time(h, k.encode(), ct.byref(tot), ct.byref(cnt))
+                if cnt.value:
+                    ks[k] = round(tot.value / cnt.value, 4)
+            res[n]["kernels_ms"] = ks
     print(json.dumps({"W": W, "H": H, "D": D, "entry": a.entry, "iters": a.iters,
                       "variants": res}), flush=True)
     for n, lib, h in handles:
