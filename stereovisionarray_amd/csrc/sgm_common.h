@@ -162,7 +162,7 @@ struct Edges {
     unsigned X = INF2, Y = INF2;
 };
 
-template <int DPL>
+template <int DPL, bool PIN = false>
 __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigned (&A)[DPL / 2],
                                            unsigned& m, unsigned (&ow)[DPL / 4], unsigned P1,
                                            unsigned P2, Edges& e) {
@@ -213,7 +213,7 @@ __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigne
         }
     }
     const u16x2 mf = as_v2(mm[0]);
-    m = row_min_u32(mf.x < mf.y ? mf.x : mf.y);
+    m = row_min_u32<PIN>(mf.x < mf.y ? mf.x : mf.y);
 }
 
 template <int DPL>
@@ -225,14 +225,14 @@ __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigne
 }
 
 // The same step on u8-packed cost words (DPL/4 dwords of 4 disparities).
-template <int DPL>
+template <int DPL, bool PIN = false>
 __device__ __forceinline__ void sgm_step(const unsigned (&cw)[DPL / 4], unsigned (&A)[DPL / 2],
                                          unsigned& m, unsigned (&ow)[DPL / 4], unsigned P1,
                                          unsigned P2, Edges& e) {
     unsigned c[DPL / 2];
 #pragma unroll
     for (int w = 0; w < DPL / 4; w++) unpack4(cw[w], c[2 * w], c[2 * w + 1]);
-    sgm_step_c<DPL>(c, A, m, ow, P1, P2, e);
+    sgm_step_c<DPL, PIN>(c, A, m, ow, P1, P2, e);
 }
 
 // Direction table, identical to oracle svo_direction().
@@ -420,7 +420,7 @@ __device__ __forceinline__ void unpack_add(const unsigned (&w)[NW], unsigned (&S
 // checkpoint truncated; they restart at 255.  Every real disparity evolves
 // the same from 255 as from the true value: a padded neighbour enters only
 // as A + P1 >= 255 >= m + P2 (m <= 62), and never sets the row minimum.
-template <int DPL, bool PAD>
+template <int DPL, bool PAD, bool PIN = false>
 __device__ __forceinline__ void state_from_words(const Words<DPL / 4>& w, unsigned (&A)[DPL / 2],
                                                  unsigned& m, const unsigned (&padm)[DPL / 2]) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
@@ -437,12 +437,12 @@ __device__ __forceinline__ void state_from_words(const Words<DPL / 4>& w, unsign
         mm = mm < lo ? mm : lo;
         mm = mm < hi ? mm : hi;
     }
-    m = row_min_u32(mm);
+    m = row_min_u32<PIN>(mm);
 }
-template <int DPL, bool PAD>
+template <int DPL, bool PAD, bool PIN = false>
 __device__ __forceinline__ void load_state(rsrc_t r, unsigned off, unsigned (&A)[DPL / 2],
                                            unsigned& m, const unsigned (&padm)[DPL / 2]) {
-    state_from_words<DPL, PAD>(bload<DPL / 4>(r, off), A, m, padm);
+    state_from_words<DPL, PAD, PIN>(bload<DPL / 4>(r, off), A, m, padm);
 }
 
 }  // namespace sgm

@@ -37,6 +37,10 @@ __device__ __forceinline__ unsigned row_shl1(unsigned v, unsigned edge) {
 }
 
 // Minimum over the 16 lanes of a DPP row, result broadcast to all 16 lanes.
+// PIN: keep the last min next to its DPP move (an empty asm on the result), so
+// that it folds into one v_min_u32_dpp; unpinned, the compiler may sink it past
+// a caller's branch and emit v_mov 0 + v_mov_dpp + v_min.
+template <bool PIN = false>
 __device__ __forceinline__ unsigned row_min_u32(unsigned v) {
     unsigned x;
     x = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_QUAD_1032, 0xf, 0xf, false);
@@ -47,6 +51,7 @@ __device__ __forceinline__ unsigned row_min_u32(unsigned v) {
     v = v < x ? v : x;
     x = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_MIRROR, 0xf, 0xf, false);
     v = v < x ? v : x;
+    if constexpr (PIN) asm("" : "+v"(v));
     return v;
 }
 

@@ -64,6 +64,15 @@ constexpr int kWtahvRowCFirst = 1;
 // per SIMD (D=192: 157 -> 169 VGPRs).
 constexpr int kWtahvKeepU16 = 1;
 constexpr int kWtahvKeepU16Wide = 0;
+// The row minimum's last DPP step pinned next to its move (sva_device.h
+// row_min_u32<true>: one v_min_u32_dpp instead of v_mov 0 + v_mov_dpp + v_min),
+// in the recurrences and in the WTA.  wta_hv, in-process, 3 variants x 2
+// positions (profiles/r03_v8/ab_wtahv_pin_row_min.log.txt): 1080p D=128
+// 0.2599 / 0.2667 -> 0.2586 / 0.2657 ms, 4K D=256 2.314 -> 2.284 ms; small but
+// the same sign at every D.  (In sgm_paths the same pin was neutral at 1080p
+// and 1-2 % slower at 4K, so the path kernel stays unpinned.)
+constexpr int kWtahvPinRowMin = 1;
+constexpr int kWtahvPinWta = 1;
 
 // ---- census.hip / census_cost.hip / cost.hip ------------
 // Rows per workgroup of the multi-row census kernel.

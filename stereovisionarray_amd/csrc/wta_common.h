@@ -39,7 +39,7 @@ __device__ __forceinline__ float subpixel(int dmin, int ds, int D, unsigned a, u
 // adjacent pairs: each lane selects pair q = (d*-1-d0) >> 1 and q + 1 of
 // its own (zero outside the lane) and one v_perm packs the two halves; a
 // single DPP OR-reduction then gathers both values.
-template <int DPL>
+template <int DPL, bool PIN = false>
 __device__ __forceinline__ int wta_pick_raw(const unsigned (&S)[DPL / 2], int k, bool want_sub,
                                             unsigned* spm, unsigned* s0) {
     constexpr int NP = DPL / 2;
@@ -52,7 +52,7 @@ __device__ __forceinline__ int wta_pick_raw(const unsigned (&S)[DPL / 2], int k,
         best = best < lo ? best : lo;
         best = best < hi ? best : hi;
     }
-    best = row_min_u32(best);
+    best = row_min_u32<PIN>(best);
     const int ds = (int)(best & 0xffffu);
     if (want_sub) {
         const int im = ds - 1 - d0;             // local index of d*-1 (may leave the lane)

@@ -58,6 +58,8 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
     constexpr int NW = DPL / 4, NP = DPL / 2;
     constexpr int TY = 1 << TYL;        // tile rows = checkpoint segment (rows and columns)
     constexpr bool KEEP16 = DPL <= 8 ? tune::kWtahvKeepU16 != 0 : tune::kWtahvKeepU16Wide != 0;
+    constexpr bool PIN = tune::kWtahvPinRowMin != 0;     // row_min_u32<PIN>
+
     constexpr int SPR = TW / TY;        // phase H: row segments per tile row
     static_assert(TY <= TW && TW % TY == 0, "tile rows must divide 16");
     const int tx = (int)(blockIdx.x % (unsigned)g.ntx);
@@ -119,12 +121,12 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
     // chains per wave).
     if (vcol) {
         if (ty > 0)
-            load_state<DPL, PAD>(make_rsrc(CKV, g.vck), ((unsigned)(ty - 1) * uW + xv) * uD + lane_d,
+            load_state<DPL, PAD, PIN>(make_rsrc(CKV, g.vck), ((unsigned)(ty - 1) * uW + xv) * uD + lane_d,
                                  Aa, ma, padm);
         else
             zero_state(Aa, ma);
         if (y0 + TY < H)
-            load_state<DPL, PAD>(make_rsrc(CKV + g.vck, g.vck),
+            load_state<DPL, PAD, PIN>(make_rsrc(CKV + g.vck, g.vck),
                                  ((unsigned)(ty + 1) * uW + xv) * uD + lane_d, Ab, mb, padm);
         else
             zero_state(Ab, mb);
@@ -157,8 +159,8 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
             for_seq<TY>([&](auto I) {
                 constexpr int i = decltype(I)::value, ru = TY - 1 - i;
                 unsigned ow[NW];
-                if (i < ny) { sgm_step<DPL>(cv[i].w, Aa, ma, ow, P1, P2, ea); keep(LD[i], Aa, ow); }
-                if (ru < ny) { sgm_step<DPL>(cv[ru].w, Ab, mb, ow, P1, P2, eb); keep(LU[ru], Ab, ow); }
+                if (i < ny) { sgm_step<DPL, PIN>(cv[i].w, Aa, ma, ow, P1, P2, ea); keep(LD[i], Aa, ow); }
+                if (ru < ny) { sgm_step<DPL, PIN>(cv[ru].w, Ab, mb, ow, P1, P2, eb); keep(LU[ru], Ab, ow); }
             });
             for_seq<TY>([&](auto R) {
                 constexpr int r = decltype(R)::value;
@@ -176,13 +178,13 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
             for_seq<TY>([&](auto I) {
                 constexpr int i = decltype(I)::value;
                 unsigned ow[NW];
-                if (i < ny) { sgm_step<DPL>(cv[i].w, Aa, ma, ow, P1, P2, ea); keep(LD[i], Aa, ow); }
+                if (i < ny) { sgm_step<DPL, PIN>(cv[i].w, Aa, ma, ow, P1, P2, ea); keep(LD[i], Aa, ow); }
             });
             for_seq<TY>([&](auto Q) {
                 constexpr int r = TY - 1 - decltype(Q)::value;
                 if (r < ny) {
                     unsigned lu[NW];
-                    sgm_step<DPL>(cv[r].w, Ab, mb, lu, P1, P2, eb);
+                    sgm_step<DPL, PIN>(cv[r].w, Ab, mb, lu, P1, P2, eb);
                     put_v(r, LD[r], Ab, lu);
                 }
             });
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
     // the sum and the WTA per pixel
     if (!hrow) return;                                 // whole 16-lane row leaves together
     if constexpr (tune::kWtahvEarlyLoads == 0) issue_first();
-    if (hs > 0) state_from_words<DPL, PAD>(ckw[0], Aa, ma, padm);
+    if (hs > 0) state_from_words<DPL, PAD, PIN>(ckw[0], Aa, ma, padm);
     else zero_state(Aa, ma);
     // L_0 of the segment's pixels, kept like phase V's L_2 (KEEP16)
     constexpr int NKH = KEEP16 ? NP : NW;
@@ -229,12 +231,12 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
         constexpr int i = decltype(I)::value;
         unsigned ow[NW];
         if (i < nh) {
-            sgm_step<DPL>(ch[i].w, Aa, ma, ow, P1, P2, ea);
+            sgm_step<DPL, PIN>(ch[i].w, Aa, ma, ow, P1, P2, ea);
 #pragma unroll
             for (int q = 0; q < NKH; q++) LF[i][q] = KEEP16 ? Aa[q] : ow[q];
         }
     });
-    if (hx + TY < W) state_from_words<DPL, PAD>(ckw[1], Aa, ma, padm);
+    if (hx + TY < W) state_from_words<DPL, PAD, PIN>(ckw[1], Aa, ma, padm);
     else zero_state(Aa, ma);
     unsigned dres = 0u, sm = 0u, s0 = 0u;
     const bool want_sub = sub != nullptr;
@@ -242,7 +244,7 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
         constexpr int q = decltype(Q)::value, j = TY - 1 - q, s = q % kPfVol;
         if (j < nh) {
             unsigned ow[NW];
-            sgm_step<DPL>(ch[j].w, Aa, ma, ow, P1, P2, ea);
+            sgm_step<DPL, PIN>(ch[j].w, Aa, ma, ow, P1, P2, ea);
             const unsigned* vs = &vsum[((hr * TW + hseg * TY + j) * 16 + k) * NP];
             unsigned S[NP];
 #pragma unroll
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
                 for (int p = 0; p < NP; p++) S[p] |= padm[p];
             }
             unsigned spm, sb;
-            const int ds = wta_pick_raw<DPL>(S, k, want_sub, &spm, &sb);
+            const int ds = wta_pick_raw<DPL, PIN && tune::kWtahvPinWta>(S, k, want_sub, &spm, &sb);
             if (k == j) {
                 dres = (unsigned)ds;
                 sm = spm;
