@@ -27,7 +27,8 @@ namespace sva {
 namespace {
 
 constexpr int CC_BLOCK = 256;
-constexpr int PXB = tune::kCensusCostPx;   // pixels per workgroup row
+// pixels per workgroup row, per disparity width (tune::kCensusCostPx*)
+template <int NC> constexpr int pxb_of() { return NC > 8 ? tune::kCensusCostPxWide : tune::kCensusCostPx; }
 constexpr int RING = 8;              // image rows in LDS (power of two)
 constexpr int HX = 4, HY = 3;        // half window (9 wide, 7 high)
 constexpr uint64_t kOutsideCC = 1ull << 63;   // never set in a census word (bits 0..61)
@@ -51,6 +52,7 @@ __global__ __launch_bounds__(CC_BLOCK) void census_cost_kernel(
     const uint8_t* __restrict__ left, const uint8_t* __restrict__ right, int W, int H,
     size_t pitch, int dmin, int dir, int rows, int dreal, uint8_t* __restrict__ C) {
     constexpr int D = NC * 16;
+    constexpr int PXB = pxb_of<NC>();
     constexpr int NW = PXB + D - 1;                      // right census words per row
     constexpr int RW = (NW + 8 + 4 + 3) / 4 * 4;         // right ring row bytes (+ dword overrun)
     constexpr int LW = (PXB + 8 + 4 + 3) / 4 * 4;        // left ring row bytes
@@ -208,6 +210,7 @@ hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right,
     if (dreal <= 0) dreal = D;
     ScopedKernelTimer t(c, "cost");
     const int rows = tune::kCensusCostRows;
+    const int PXB = D > 128 ? pxb_of<16>() : pxb_of<8>();
     const int bpr = (W + PXB - 1) / PXB;
     const dim3 grid((unsigned)(bpr * ((H + rows - 1) / rows)));
     const int sd = dir > 0 ? 1 : -1;

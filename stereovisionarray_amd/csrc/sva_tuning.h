@@ -82,6 +82,11 @@ constexpr int kCensusRows = 16;
 // D=128, profiles/r01_v8/ab_census_cost_tiling.jsonl); 192 / 256 px measured
 // 0.093 / 0.101 ms in round 2.
 constexpr int kCensusCostPx = 128;
+// D > 128 on its own constant: 192 / 256 px form 25-37 % fewer census words
+// there, yet census_cost ran slower in round 3 (1080p D=256 0.149 -> 0.184 /
+// 0.193 ms, D=192 0.123 -> 0.139 / 0.145 ms, 4K D=256 0.705 -> 0.713 / 0.732
+// ms; profiles/r03_v8/ab_census_cost_wide_tiles.log.txt).
+constexpr int kCensusCostPxWide = 128;
 constexpr int kCensusCostRows = 4;
 // Cost-volume stores of census_cost: 1 non-temporal, 0 default policy.
 constexpr int kCostStoreNT = 1;
