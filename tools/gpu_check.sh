@@ -28,6 +28,8 @@ for step in "$@"; do
     batch_gloo2) run batch_gloo2 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 --workload batch256_d192 --steps 1 --warmup 1 --dist-backend gloo ;;
     array_gloo2) run center8_gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --workload center8 --steps 3 --warmup 1 --dist-backend gloo ;;
     rccl1) run bench_rccl1 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --rehearse-rccl ;;
+    engine) run bench_engine_n1 600 python bench.py --engine multi --steps 10 --warmup 3 --no-cpu-baseline
+            run bench_engine_batch256 900 python bench.py --engine multi --workload batch256_d192 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench_test) run bench_test 600 python -u -m pytest tests/test_bench_gpu.py -q -m gpu --timeout 300 --timeout-method thread ;;
     bench4k) run bench4k 600 python bench.py --steps 5 --warmup 2 --workload 4k_d256 --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
