@@ -58,8 +58,14 @@ ARRAY_PS = 0.036 / 1920        # m / pixel
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 100; 20 for the 256-pair batch workload)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps before them (default 50; 5 for the batch workload). "
+                         "The first ~20 frames after start-up run 3-4 %% slow (clocks, first "
+                         "touches): with 5 warmups a 20-step run measured 0.935 ms per 1080p "
+                         "frame, with 50 warmups 0.897 and 200 steps 0.892 "
+                         "(profiles/r03_v8/bench_warmup_probe.log.txt)")
     ap.add_argument("--workload", default="1080p_d128", choices=sorted(WORKLOADS))
     ap.add_argument("--pairs-per-rank", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -89,7 +95,13 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (real runs); gloo = rehearsal with ranks "
                          "sharing one GPU, maps gathered through host memory")
-    return ap.parse_args()
+    a = ap.parse_args()
+    batch = "total_pairs" in WORKLOADS[a.workload]
+    if a.steps is None:
+        a.steps = 20 if batch else 100
+    if a.warmup is None:
+        a.warmup = 5 if batch else 50
+    return a
 
 
 def host_cpu():
