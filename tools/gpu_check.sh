@@ -19,7 +19,7 @@ for step in "$@"; do
     pytest) run pytest_gpu 1200 python -u -m pytest tests -q -m "gpu and not slow" -x --timeout 120 --timeout-method thread ;;
     pytest_all) run pytest_gpu_all 1500 python -u -m pytest tests -q -m gpu -rf --timeout 300 --timeout-method thread ;;
     pytest_slow) run pytest_gpu_slow 900 python -u -m pytest tests -v -m "gpu and slow" -rf --timeout 300 --timeout-method thread ;;
-    bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    bench) run bench 600 python bench.py ;;
     pytest_array) run pytest_array 900 python -m pytest tests/test_array_gpu.py -q -m gpu ;;
     array) run center8 600 python bench.py --workload center8 --steps 5 --warmup 2 --no-cpu-baseline
            run grid8_all 600 python bench.py --workload grid8_all --steps 5 --warmup 2 --no-cpu-baseline ;;
