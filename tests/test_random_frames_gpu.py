@@ -86,3 +86,46 @@ def test_random_frame_2d_step(ctx, sva, oracle, case):
     assert bad == 0, f"{bad} of {W * H} pixels differ (W={W} H={H} D={D} dmin={dmin} " \
                      f"step=({sx},{sy}) P1={P1} P2={P2})"
     assert np.max(np.abs(sub - osub)) <= SUB_TOL
+
+
+def _cases_ref(n=32, seed=20261019):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        W, H = int(rng.integers(48, 480)), int(rng.integers(40, 360))
+        ref = int(rng.integers(0, 25))
+        oth = ref
+        while oth == ref:
+            oth = int(rng.integers(0, 25))
+        k = int(rng.integers(1, min(33, min(W, H) // 3)))
+        # keep the single-threaded oracle to a second or two: W*H pixels x
+        # ~W/4 candidates x (2k)^2 absolute differences
+        while W * H * (W // 4) * 4 * k * k > 8e9 and min(W, H) > 48:
+            W, H = W * 3 // 4, H * 3 // 4
+        k = min(k, min(W, H) // 3)
+        masked = bool(rng.random() < 0.4)
+        shift = int(rng.integers(0, 24))
+        out.append((i, W, H, ref, oth, k, masked, shift))
+    return out
+
+
+@pytest.mark.parametrize("case", _cases_ref(), ids=lambda c: "r%02d_%dx%d_%d-%d_k%d" % c[:6])
+def test_random_mode_r(ctx, sva, oracle, case):
+    """Mode R, the reference's own path (CameraStereoVision.cpp:44-95): any
+    camera pair of the 5x5 rig (Low and High Bresenham lines, both signs,
+    long baselines), any window 1 <= k <= 32, with and without a mask;
+    valid, the u8-wrapped and the u16 maps bit-exact vs the oracle."""
+    i, W, H, ref, oth, k, masked, shift = case
+    ps = 0.036 / W
+    grid = synth.reference_array(ps)
+    cr, co = sva.Camera.make(*grid[ref]), sva.Camera.make(*grid[oth])
+    ocr, oco = oracle.OCamera.make(*grid[ref]), oracle.OCamera.make(*grid[oth])
+    a = synth.texture(H, W, 3000 + i)
+    b = np.roll(a, shift, axis=int(i % 2))
+    mask = None
+    if masked:
+        mask = (synth.texture(H, W, 4000 + i) > 96).astype(np.uint8) * 255
+    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k, mask=mask)
+    o8, o16, ovalid, _ = oracle.ref_pair(a, b, ocr, oco, k=k, mask=mask)
+    assert np.array_equal(valid, ovalid), f"{int((valid != ovalid).sum())} valid flags differ"
+    assert np.array_equal(d16, o16) and np.array_equal(d8, o8)
