@@ -31,7 +31,7 @@ for step in "$@"; do
     engine) run bench_engine_n1 600 python bench.py --engine multi --steps 10 --warmup 3 --no-cpu-baseline
             run bench_engine_batch256 900 python bench.py --engine multi --workload batch256_d192 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench_test) run bench_test 600 python -u -m pytest tests/test_bench_gpu.py -q -m gpu --timeout 300 --timeout-method thread ;;
-    bench4k) run bench4k 600 python bench.py --steps 5 --warmup 2 --workload 4k_d256 --no-cpu-baseline ;;
+    bench4k) run bench4k 600 python bench.py --workload 4k_d256 --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;

@@ -16,8 +16,8 @@ def main():
     import torch
     import stereovisionarray_amd as sva
     from stereovisionarray_amd import synth
-    W, H, D = 1920, 1080, 128
     frames, rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 20, 8
+    W, H, D = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1920, 1080, 128)
     dev = torch.device("cuda", 0)
     L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=1)
     dL, dR = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
@@ -48,7 +48,18 @@ def main():
     for _ in range(rounds):
         for m in (0, 2, 1):
             res[m].append(run(m))
-    print(json.dumps({"frames_per_run": frames, "rounds": rounds,
+    # one isolated frame (host sync before and after), as tools/ab_paths.py times them
+    iso = []
+    for _ in range(rounds):
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        ctx.disparity_sgm_d(dL.data_ptr(), dR.data_ptr(), W, H, W, p, disp.data_ptr(), sub.data_ptr())
+        e1.record(s)
+        e1.synchronize()
+        iso.append(e0.elapsed_time(e1))
+    print(json.dumps({"W": W, "H": H, "D": D, "frames_per_run": frames, "rounds": rounds,
+                      "isolated_frame_ms_median": round(statistics.median(iso), 4),
                       "ms_per_frame_median": {f"timing_{m}": round(statistics.median(v), 4)
                                               for m, v in res.items()},
                       "ms_per_frame_min": {f"timing_{m}": round(min(v), 4) for m, v in res.items()}}))
