@@ -58,12 +58,18 @@ constexpr int kWtahvEarlyLoads = 1;
 // Phase H's cost words loaded with phase V's at the start (1) or after phase
 // V's recurrences (0).
 constexpr int kWtahvRowCFirst = 1;
-// Phase V's L_2 and phase H's L_0 kept per pixel as the step's u16 pairs (1:
-// V and S need only packed adds) or u8-packed (0: two v_perm per word to
-// re-expand, half the registers).  Above D = 128 the u16 copy costs a wave
-// per SIMD (D=192: 157 -> 169 VGPRs).
-constexpr int kWtahvKeepU16 = 1;
-constexpr int kWtahvKeepU16Wide = 0;
+// Phase V's L_2 (bit 0) and phase H's L_0 (bit 1) kept per pixel as the
+// step's u16 pairs (V and S need only packed adds) instead of u8-packed (two
+// v_perm per word to re-expand, half the registers).  D <= 128: both, wta_hv
+// 0.273 -> 0.266 ms at 1080p D=128.  Above D = 128 both copies would cost a
+// wave per SIMD (D=192: 157 -> 169 VGPRs); phase V's alone costs no register
+// (157 / 194 VGPRs at D=192 / 256, as with none) and phase H's alone keeps
+// the occupancy too, so they were measured one at a time
+// (profiles/r03_v8/ab_wtahv_keep_u16_wide.log.txt, wta_hv at 1080p): none /
+// V / H  D=192 0.4138 / 0.4096 / 0.4107 ms, D=256 0.5832 / 0.5740 / 0.5717,
+// D=150 0.3981 / 0.3903 / 0.3936, D=232 0.5805 / 0.5653 / 0.5653.
+constexpr int kWtahvKeepU16 = 3;
+constexpr int kWtahvKeepU16Wide = 1;
 // The row minimum's last DPP step pinned next to its move (sva_device.h
 // row_min_u32<true>: one v_min_u32_dpp instead of v_mov 0 + v_mov_dpp + v_min),
 // in the recurrences and in the WTA.  wta_hv, in-process, 3 variants x 2

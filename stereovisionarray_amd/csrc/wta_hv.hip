@@ -57,7 +57,9 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
                                                     float* __restrict__ sub) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
     constexpr int TY = 1 << TYL;        // tile rows = checkpoint segment (rows and columns)
-    constexpr bool KEEP16 = DPL <= 8 ? tune::kWtahvKeepU16 != 0 : tune::kWtahvKeepU16Wide != 0;
+    // bit 0: phase V keeps L_2 as u16, bit 1: phase H keeps L_0 as u16
+    constexpr int KEEPM = DPL <= 8 ? tune::kWtahvKeepU16 : tune::kWtahvKeepU16Wide;
+    constexpr bool KEEP16 = (KEEPM & 1) != 0, KEEP16H = (KEEPM & 2) != 0;
     constexpr bool PIN = tune::kWtahvPinRowMin != 0;     // row_min_u32<PIN>
 
     constexpr int SPR = TW / TY;        // phase H: row segments per tile row
@@ -224,8 +226,8 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
     if constexpr (tune::kWtahvEarlyLoads == 0) issue_first();
     if (hs > 0) state_from_words<DPL, PAD, PIN>(ckw[0], Aa, ma, padm);
     else zero_state(Aa, ma);
-    // L_0 of the segment's pixels, kept like phase V's L_2 (KEEP16)
-    constexpr int NKH = KEEP16 ? NP : NW;
+    // L_0 of the segment's pixels, kept like phase V's L_2 (KEEP16H)
+    constexpr int NKH = KEEP16H ? NP : NW;
     unsigned LF[TY][NKH];
     for_seq<TY>([&](auto I) {
         constexpr int i = decltype(I)::value;
@@ -233,7 +235,7 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
         if (i < nh) {
             sgm_step<DPL, PIN>(ch[i].w, Aa, ma, ow, P1, P2, ea);
 #pragma unroll
-            for (int q = 0; q < NKH; q++) LF[i][q] = KEEP16 ? Aa[q] : ow[q];
+            for (int q = 0; q < NKH; q++) LF[i][q] = KEEP16H ? Aa[q] : ow[q];
         }
     });
     if (hx + TY < W) state_from_words<DPL, PAD, PIN>(ckw[1], Aa, ma, padm);
@@ -249,7 +251,7 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
             unsigned S[NP];
 #pragma unroll
             for (int p = 0; p < NP; p++) S[p] = vs[p] + Aa[p];   // V + L_1
-            if constexpr (KEEP16) {
+            if constexpr (KEEP16H) {
 #pragma unroll
                 for (int p = 0; p < NP; p++) S[p] += LF[j][p];     // + L_0
             } else {

@@ -50,8 +50,14 @@ def main():
     subm = torch.zeros((H, W), dtype=torch.float32, device=dev)
     C = torch.zeros((H, W, D), dtype=torch.uint8, device=dev)
     L8 = torch.zeros((8, H, W, D), dtype=torch.uint8, device=dev)
-    ns, _ = sva.ckpt_segments(W, D)
-    CK = torch.zeros((2, H, ns, D), dtype=torch.uint8, device=dev)
+    # checkpoint planes of the ckpt / wta_h entries, full size: sva_paths_ckpt_d
+    # writes [2][H][ns][D] whatever the caller allocated.  Those stage entries
+    # take the native widths only; other D skip them.
+    native = D in (64, 128, 192, 256)
+    if a.entry in ("ckpt", "wta_h") and not native:
+        raise SystemExit(f"--entry {a.entry} needs D in 64/128/192/256")
+    ns = sva.ckpt_segments(W, D)[0] if native else 0
+    CK = torch.zeros((2, H, ns, D), dtype=torch.uint8, device=dev) if native else None
     p = sva.default_params(D=D, dmin=a.dmin, dir=a.dir, subpixel=1 if a.sub else 0)
     handles = []
     for path in a.libs:
@@ -78,8 +84,9 @@ def main():
     torch.cuda.synchronize()
     C_ref = C_src.clone()          # census -> cost bytes, checked against every census_cost variant
     # checkpoint-mode volumes for the wta_h entry (first library)
-    lib0.sva_paths_ckpt_d(h0, ct.c_void_p(C_src.data_ptr()), W, H, ct.byref(p),
-                          ct.c_void_p(L8.data_ptr()), ct.c_void_p(CK.data_ptr()))
+    if native:
+        assert lib0.sva_paths_ckpt_d(h0, ct.c_void_p(C_src.data_ptr()), W, H, ct.byref(p),
+                                     ct.c_void_p(L8.data_ptr()), ct.c_void_p(CK.data_ptr())) == 0
     torch.cuda.synchronize()
     times = {n: [] for n, _, _ in handles}
     ref = None
