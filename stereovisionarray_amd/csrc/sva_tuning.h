@@ -79,6 +79,14 @@ constexpr int kWtahvKeepU16Wide = 1;
 // and 1-2 % slower at 4K, so the path kernel stays unpinned.)
 constexpr int kWtahvPinRowMin = 1;
 constexpr int kWtahvPinWta = 1;
+// Sub-pixel neighbours S(d*-1), S(d*+1): through LDS (1: S written over the
+// pixel's dead V block, two u16 reads by the owning lane) or gathered in
+// registers (0: per-pair selects, a v_perm and a 4-step DPP OR-reduction).
+// 9 % fewer static VALU in wta_hv<8>; wta_hv in-process, 0 -> 1
+// (profiles/r03_v8/ab_wtahv_subpixel_lds.log.txt): 1080p D=128 0.2514 / 0.2529
+// -> 0.2495 / 0.2450 ms, D=64 0.150 -> 0.144, D=192 0.393 -> 0.380, D=256
+// 0.556 -> 0.538, 4K D=256 2.215 -> 2.158.
+constexpr int kWtahvSubLds = 1;
 
 // ---- census.hip / census_cost.hip / cost.hip ------------
 // Rows per workgroup of the multi-row census kernel.

@@ -70,6 +70,22 @@ __device__ __forceinline__ int wta_pick_raw(const unsigned (&S)[DPL / 2], int k,
     return ds;
 }
 
+// The first-minimum key of the row, (S(d*) << 16) | d*, in all 16 lanes.
+template <int DPL, bool PIN = false>
+__device__ __forceinline__ unsigned wta_pick_key(const unsigned (&S)[DPL / 2], int k) {
+    constexpr int NP = DPL / 2;
+    const int d0 = k * DPL;
+    unsigned best = 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+        const unsigned lo = ((S[j] & 0xffffu) << 16) | (unsigned)(d0 + 2 * j);
+        const unsigned hi = (S[j] & 0xffff0000u) | (unsigned)(d0 + 2 * j + 1);
+        best = best < lo ? best : lo;
+        best = best < hi ? best : hi;
+    }
+    return row_min_u32<PIN>(best);
+}
+
 // Returns d* (0-based, the same in all 16 lanes of the row) and, when
 // want_sub, the f32 sub-pixel disparity dmin + d* (+ parabola offset) in *v.
 template <int DPL>

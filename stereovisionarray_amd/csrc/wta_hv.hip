@@ -247,7 +247,8 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
         if (j < nh) {
             unsigned ow[NW];
             sgm_step<DPL, PIN>(ch[j].w, Aa, ma, ow, P1, P2, ea);
-            const unsigned* vs = &vsum[((hr * TW + hseg * TY + j) * 16 + k) * NP];
+            unsigned* const vpix = &vsum[(hr * TW + hseg * TY + j) * 16 * NP];   // this pixel's V
+            const unsigned* vs = vpix + k * NP;
             unsigned S[NP];
 #pragma unroll
             for (int p = 0; p < NP; p++) S[p] = vs[p] + Aa[p];   // V + L_1
@@ -264,11 +265,33 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
                 for (int p = 0; p < NP; p++) S[p] |= padm[p];
             }
             unsigned spm, sb;
-            const int ds = wta_pick_raw<DPL, PIN && tune::kWtahvPinWta>(S, k, want_sub, &spm, &sb);
-            if (k == j) {
-                dres = (unsigned)ds;
-                sm = spm;
-                s0 = sb;
+            if constexpr (tune::kWtahvSubLds != 0) {
+                // S(d*-1) and S(d*+1) through LDS: every lane writes its S
+                // pairs over the pixel's V block, which nothing reads again;
+                // as u16 the block is S indexed by d.  The owning lane reads
+                // the two neighbours (same wave: LDS keeps the order).
+                const unsigned best = wta_pick_key<DPL, PIN && tune::kWtahvPinWta>(S, k);
+                const int ds = (int)(best & 0xffffu);
+                if (want_sub) {
+#pragma unroll
+                    for (int p = 0; p < NP; p++) vpix[k * NP + p] = S[p];
+                }
+                if (k == j) {
+                    dres = (unsigned)ds;
+                    s0 = best >> 16;
+                    if (want_sub) {
+                        const uint16_t* s16 = reinterpret_cast<const uint16_t*>(vpix);
+                        const int dm = ds > 0 ? ds - 1 : 0, dp = ds + 1 < 16 * DPL ? ds + 1 : ds;
+                        sm = (unsigned)s16[dm] | ((unsigned)s16[dp] << 16);
+                    }
+                }
+            } else {
+                const int ds = wta_pick_raw<DPL, PIN && tune::kWtahvPinWta>(S, k, want_sub, &spm, &sb);
+                if (k == j) {
+                    dres = (unsigned)ds;
+                    sm = spm;
+                    s0 = sb;
+                }
             }
         }
         if constexpr (q + kPfVol < TY) {
