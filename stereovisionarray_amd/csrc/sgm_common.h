@@ -147,6 +147,31 @@ __device__ __forceinline__ unsigned min3_u16x2(unsigned a, unsigned b, unsigned 
     return r;
 }
 
+// Minimum over the 2*NP u16 halves of A (values below 1024): a tree of
+// three-input packed mins, then the two halves.
+template <int NP>
+__device__ __forceinline__ unsigned lane_min_u16(const unsigned (&A)[NP]) {
+    unsigned mm[NP];
+#pragma unroll
+    for (int j = 0; j < NP; j++) mm[j] = A[j];
+    int n = NP;
+#pragma unroll
+    for (int it = 0; it < 4; it++) {
+        if (n > 1) {
+            int o = 0, i = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                if (i + 2 < n) { mm[o++] = min3_u16x2(mm[i], mm[i + 1], mm[i + 2]); i += 3; }
+                else if (i + 1 < n) { mm[o++] = as_u32(vmin2(as_v2(mm[i]), as_v2(mm[i + 1]))); i += 2; }
+                else if (i < n) { mm[o++] = mm[i]; i += 1; }
+            }
+            n = o;
+        }
+    }
+    const u16x2 mf = as_v2(mm[0]);
+    return mf.x < mf.y ? mf.x : mf.y;
+}
+
 // One recurrence step for the lane's DPL disparities.  State A = L(q, .)
 // (unnormalised u16 pairs), m = min_k L(q, k) broadcast over the row.
 //   u      = min(min(A(d-1), A(d+1)) + P1, A(d), m + P2)      (all >= m)
@@ -194,26 +219,7 @@ __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigne
     for (int j = 0; j < NP; j++) A[j] = add3(min3_u16x2(as_u32(t[j]), A[j], mP2), c[j], K);
 #pragma unroll
     for (int w = 0; w < NW; w++) ow[w] = pack4(A[2 * w], A[2 * w + 1]);
-    // min over the lane's pairs: three-input mins, then the two halves
-    unsigned mm[NP];
-#pragma unroll
-    for (int j = 0; j < NP; j++) mm[j] = A[j];
-    int n = NP;
-#pragma unroll
-    for (int it = 0; it < 4; it++) {
-        if (n > 1) {
-            int o = 0, i = 0;
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                if (i + 2 < n) { mm[o++] = min3_u16x2(mm[i], mm[i + 1], mm[i + 2]); i += 3; }
-                else if (i + 1 < n) { mm[o++] = as_u32(vmin2(as_v2(mm[i]), as_v2(mm[i + 1]))); i += 2; }
-                else if (i < n) { mm[o++] = mm[i]; i += 1; }
-            }
-            n = o;
-        }
-    }
-    const u16x2 mf = as_v2(mm[0]);
-    m = row_min_u32<PIN>(mf.x < mf.y ? mf.x : mf.y);
+    m = row_min_u32<PIN>(lane_min_u16<NP>(A));
 }
 
 template <int DPL>
@@ -430,14 +436,18 @@ __device__ __forceinline__ void state_from_words(const Words<DPL / 4>& w, unsign
 #pragma unroll
         for (int j = 0; j < NP; j++) A[j] |= padm[j] & 0x00ff00ffu;   // A < 256: OR = max
     }
-    unsigned mm = 0xffffffffu;
+    if constexpr (tune::kStateMinTree) {
+        m = row_min_u32<PIN>(lane_min_u16<NP>(A));
+    } else {
+        unsigned mm = 0xffffffffu;
 #pragma unroll
-    for (int j = 0; j < NP; j++) {
-        const unsigned lo = A[j] & 0xffffu, hi = A[j] >> 16;
-        mm = mm < lo ? mm : lo;
-        mm = mm < hi ? mm : hi;
+        for (int j = 0; j < NP; j++) {
+            const unsigned lo = A[j] & 0xffffu, hi = A[j] >> 16;
+            mm = mm < lo ? mm : lo;
+            mm = mm < hi ? mm : hi;
+        }
+        m = row_min_u32<PIN>(mm);
     }
-    m = row_min_u32<PIN>(mm);
 }
 template <int DPL, bool PAD, bool PIN = false>
 __device__ __forceinline__ void load_state(rsrc_t r, unsigned off, unsigned (&A)[DPL / 2],

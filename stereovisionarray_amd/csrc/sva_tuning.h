@@ -34,6 +34,13 @@ constexpr int kCLoadAux = 0;
 // min 0.948 vs 0.942 -- noise (profiles/r03_v6/ab_retune_sgm.log.txt).
 constexpr int kCkptStoreAux = 0;
 
+// Minimum of a path state restored from a checkpoint (sgm_common.h
+// state_from_words): the packed-u16 min tree of the recurrence step (1) or
+// one scalar min per half (0).  -104 static VALU in wta_hv<8>; wta_hv
+// within 1 % either way, never slower beyond noise
+// (profiles/r03_v8/ab_state_min_tree.log.txt).
+constexpr int kStateMinTree = 1;
+
 // ---- wta_h.hip --------------------------------------------
 // Prefetch depth (steps) of the forward pass (1 cost load per step) and the
 // backward pass (6 volume loads per step); D > 128 halves the forward ring
