@@ -778,7 +778,7 @@ def run_engine(a, wl):
         subpixel = 1
     n_units = len(units)
     per_dev = -(-n_units // N)
-    S = a.streams if a.streams > 0 else (1 if per_dev == 1 or D == 192 else 2)
+    S = a.streams if a.streams > 0 else (1 if per_dev == 1 else 2)
     m = sva.Multi(list(range(N)), streams=S, flags=sva.SVA_MULTI_GATHER_RCCL)
     ctxs = [m.context(d, s) for d in range(N) for s in range(S)]
     for c in ctxs:
@@ -955,10 +955,12 @@ def main():
             raise SystemExit("total_pairs must divide evenly over the ranks")
         P = wl["total_pairs"] // world
     params = sva.default_params(D=D, dmin=0, dir=-1, subpixel=1)
-    # Pairs overlap on 2 streams by default; at D=192 a second stream loses
-    # (1080p x 256 pairs: 1 stream 251.5K, 2 streams 244.1K Mdisp/s), at D=128
-    # and D=256 it gains 4 % / 2 % (profiles/r02_v9/streams_ab.txt).
-    n_streams = a.streams if a.streams > 0 else (1 if P == 1 or D == 192 else 2)
+    # Pairs overlap on 2 streams by default.  Round 2 kept D=192 on one stream
+    # (1080p x 256 pairs: 1 stream 251.5K, 2 streams 244.1K Mdisp/s,
+    # profiles/r02_v9/streams_ab.txt); with the tile pipeline
+    # two streams win there too: 304.9-307.7K -> 317.9K Mdisp/s
+    # (profiles/r03_v8/streams_batch256.log.txt).
+    n_streams = a.streams if a.streams > 0 else (1 if P == 1 else 2)
     ctx = sva.Context(local)
     stream = torch.cuda.Stream(dev)     # non-default stream shared by kernels, copies, RCCL
     torch.cuda.set_stream(stream)
