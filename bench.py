@@ -550,8 +550,11 @@ def run_array(a, wl, world, rank, local, dev):
     nvalid = torch.zeros((len(groups), H, W), dtype=torch.uint8, device=dev)
     maps = {"all": None}
     # pairs alternate over n_streams contexts (own stream and workspaces) so
-    # consecutive pairs overlap; gather and fusion wait for all of them
-    n_streams = a.streams if a.streams > 0 else (2 if len(jobs) > 1 else 1)
+    # consecutive pairs overlap; gather and fusion wait for all of them.
+    # Three streams (profiles/r03_v8/streams_arrays.log.txt, one box): center8
+    # 311.2-315.0K (2) -> 319.7-321.0K (3) -> 309.3K (4) Mdisp/s; grid8_all
+    # 316.2-316.9K (2) -> 316.4-318.1K (3) -> 305.2-308.1K (4).
+    n_streams = a.streams if a.streams > 0 else (min(3, len(jobs)) if len(jobs) > 1 else 1)
     ctxs, cstreams = [ctx], [stream]
     for _ in range(1, n_streams):
         s_ = torch.cuda.Stream(dev)
