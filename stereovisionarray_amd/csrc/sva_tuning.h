@@ -57,7 +57,14 @@ constexpr int kWtahLdsPix = 0;
 constexpr int kWtahvTileLog2 = 3;
 constexpr int kWtahvTileLog2Wide = 3;      // D > 128
 // Prefetch depth (pixels) of the four diagonal-volume loads in the last pass.
-constexpr int kWtahvPfVol = 4;
+// Re-checked after the late-round-3 VALU cuts (profiles/r03_v8/ab_wtahv_pf_vol.log.txt,
+// wta_hv ms for 4 / 2 / 3 / 6): D=128 0.2615-0.2618 / 0.2641-0.2659 /
+// 0.2603-0.2605 / 0.293; D=192 0.4031 / 0.4048 / 0.4008 / 0.514; D=256 0.5559 /
+// 0.5129 / 0.5254 / 0.575.  D=64 keeps 4: 3 there cost 12 % (0.145 -> 0.163
+// ms, ab_wtahv_pf_vol_keep.log.txt).
+constexpr int kWtahvPfVol = 3;             // D=128, D=192
+constexpr int kWtahvPfVol4 = 4;            // D=64
+constexpr int kWtahvPfVol16 = 2;           // D=256
 // Phase V's opposite recurrences one after the other (0) or interleaved (1).
 constexpr int kWtahvInterleaveV = 0;
 // Phase H's checkpoint and first volume loads issued before the barrier.
@@ -74,9 +81,13 @@ constexpr int kWtahvRowCFirst = 1;
 // the occupancy too, so they were measured one at a time
 // (profiles/r03_v8/ab_wtahv_keep_u16_wide.log.txt, wta_hv at 1080p): none /
 // V / H  D=192 0.4138 / 0.4096 / 0.4107 ms, D=256 0.5832 / 0.5740 / 0.5717,
-// D=150 0.3981 / 0.3903 / 0.3936, D=232 0.5805 / 0.5653 / 0.5653.
+// D=150 0.3981 / 0.3903 / 0.3936, D=232 0.5805 / 0.5653 / 0.5653.  The
+// shorter volume prefetch at D >= 192 (kWtahvPfVol*) then left room for both
+// (D=192 154-161 VGPRs, 3 waves/SIMD): V+H vs V, wta_hv D=192 0.3806-0.3813
+// vs 0.3966-0.4018 ms, D=256 0.5053 vs 0.5125, 4K 1.995 vs 2.015
+// (ab_wtahv_pf_vol_keep.log.txt).
 constexpr int kWtahvKeepU16 = 3;
-constexpr int kWtahvKeepU16Wide = 1;
+constexpr int kWtahvKeepU16Wide = 3;
 // The row minimum's last DPP step pinned next to its move (sva_device.h
 // row_min_u32<true>: one v_min_u32_dpp instead of v_mov 0 + v_mov_dpp + v_min),
 // in the recurrences and in the WTA.  wta_hv, in-process, 3 variants x 2

@@ -46,7 +46,9 @@ struct WtaHvGeom {
 };
 
 // Prefetch depth (pixels) of the diagonal volumes in the last pass.
-constexpr int kPfVol = tune::kWtahvPfVol;
+template <int DPL> constexpr int pf_vol() {
+    return DPL >= 16 ? tune::kWtahvPfVol16 : DPL <= 4 ? tune::kWtahvPfVol4 : tune::kWtahvPfVol;
+}
 
 template <int DPL, int TYL, bool PAD>
 __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ C,
@@ -57,6 +59,7 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
                                                     float* __restrict__ sub) {
     constexpr int NW = DPL / 4, NP = DPL / 2;
     constexpr int TY = 1 << TYL;        // tile rows = checkpoint segment (rows and columns)
+    constexpr int kPfVol = pf_vol<DPL>();
     // bit 0: phase V keeps L_2 as u16, bit 1: phase H keeps L_0 as u16
     constexpr int KEEPM = DPL <= 8 ? tune::kWtahvKeepU16 : tune::kWtahvKeepU16Wide;
     constexpr bool KEEP16 = (KEEPM & 1) != 0, KEEP16H = (KEEPM & 2) != 0;
