@@ -112,12 +112,15 @@ int sva_reserve(void* ctx, int width, int height, int D);
 int sva_set_path_kernel(void* ctx, int kernel);
 
 /* Kernel timing with hipEvents on the context stream (measurement only).
- * enable: SVA_TIMING_OFF, SVA_TIMING_ALL (every launch), or SVA_TIMING_PATHS
- * (only the path-aggregation launch "sgm_paths": two event records per frame
- * instead of eight; each record costs a few microseconds of stream time). */
+ * enable: SVA_TIMING_OFF, SVA_TIMING_ALL (every launch), SVA_TIMING_PATHS
+ * (only the path-aggregation launch "sgm_paths") or SVA_TIMING_AGG
+ * ("sgm_paths" and "wta_hv", the two kernels of the aggregation).  The
+ * aggregation kernels are timed by their own dispatch's start/stop events;
+ * each timed launch still costs a few microseconds of stream time. */
 #define SVA_TIMING_OFF 0
 #define SVA_TIMING_ALL 1
 #define SVA_TIMING_PATHS 2
+#define SVA_TIMING_AGG 3
 int sva_set_timing(void* ctx, int enable);
 int sva_reset_timing(void* ctx);
 /* Total milliseconds and launch count of kernel `name` since the last reset. */

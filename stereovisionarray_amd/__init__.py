@@ -33,6 +33,9 @@ SVA_PATH_KERNEL_AUTO = 2
 SVA_TIMING_OFF = 0
 SVA_TIMING_ALL = 1
 SVA_TIMING_PATHS = 2
+SVA_TIMING_AGG = 3
+# The ABI this binding is written against (include/sva.h SVA_ABI_VERSION).
+ABI_VERSION = 4
 
 # Symbols declared in include/sva.h (checked by tests/test_abi.py).
 EXPORTED = [
@@ -201,6 +204,11 @@ def _load() -> ct.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # a stale build exports the same symbols with other semantics: refuse it
+    have = lib.sva_abi_version()
+    if have != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} implements ABI v{have}, this binding needs v{ABI_VERSION}: "
+                          "rebuild it (python -c 'import __graft_entry__ as g; g.build()')")
     return lib
 
 
@@ -305,7 +313,8 @@ class Context:
         self._chk(lib.sva_set_path_kernel(self.h, kernel))
 
     def set_timing(self, on):
-        """on: False/True, or SVA_TIMING_PATHS to time only the path kernel."""
+        """on: False/True, SVA_TIMING_PATHS (the path kernel only) or SVA_TIMING_AGG
+        (the path kernel and wta_hv, the two aggregation kernels)."""
         self._chk(lib.sva_set_timing(self.h, int(on)))
 
     def reset_timing(self):

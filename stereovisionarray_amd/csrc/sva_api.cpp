@@ -449,7 +449,8 @@ int sva_reserve(void* ctx, int W, int H, int D) {
     SVA_HIP(c, c->census_l.ensure(np * 8), "reserve");
     SVA_HIP(c, c->census_r.ensure(np * 8), "reserve");
     SVA_HIP(c, c->cost.ensure(nv), "reserve");
-    SVA_HIP(c, c->paths.ensure(nv * 6), "reserve");
+    // the frame route's path volumes: 4 diagonal directions (tile pipeline)
+    SVA_HIP(c, c->paths.ensure(nv * (use_tiles(W, H, D) ? 4 : 6)), "reserve");
     size_t ck = ckpt_bytes(W, H, D);                  // stage API / wta_h route
     if (use_tiles(W, H, D)) {                         // the tile pipeline's frames
         const TileGeom tg = tile_geom(W, H, D);
@@ -473,10 +474,10 @@ int sva_set_path_kernel(void* ctx, int kernel) {
 int sva_set_timing(void* ctx, int enable) {
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
-    if (enable < 0 || enable > SVA_TIMING_PATHS)
-        return fail(c, SVA_ERR_INVALID_ARG, "timing mode must be 0, 1 or 2");
+    if (enable < 0 || enable > SVA_TIMING_AGG)
+        return fail(c, SVA_ERR_INVALID_ARG, "timing mode must be 0, 1, 2 or 3");
     c->timer.enabled = enable != 0;
-    c->timer.paths_only = enable == SVA_TIMING_PATHS;
+    c->timer.mode = enable;
     return SVA_OK;
 }
 

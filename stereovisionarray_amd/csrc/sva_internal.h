@@ -26,7 +26,7 @@ struct Status {
 // while timing is enabled; resolution happens lazily in kernel_time().
 struct KernelTimer {
     bool enabled = false;
-    bool paths_only = false;   // sva_set_timing(ctx, SVA_TIMING_PATHS): path kernels only
+    int mode = 0;              // SVA_TIMING_ALL / _PATHS / _AGG (sva_set_timing)
     struct Pending {
         std::string name;
         hipEvent_t start, stop;
@@ -69,9 +69,16 @@ struct Ctx {
     std::shared_ptr<void> batch_lane;
 };
 
-// The path-aggregation launch "sgm_paths", the only one SVA_TIMING_PATHS times
-// (the roofline-graded kernel, bench.py).
-inline bool is_path_kernel(const char* name) { return std::strcmp(name, "sgm_paths") == 0; }
+// Which launches a timing mode records: SVA_TIMING_ALL every one,
+// SVA_TIMING_PATHS only the path-aggregation launch "sgm_paths" (the
+// roofline-graded kernel), SVA_TIMING_AGG that one and the kernel that
+// finishes the aggregation, "wta_hv" (bench.py's aggregation roofline).
+inline bool timer_wants(const KernelTimer& t, const char* name) {
+    if (!t.enabled) return false;
+    if (t.mode == SVA_TIMING_ALL) return true;
+    if (std::strcmp(name, "sgm_paths") == 0) return true;
+    return t.mode == SVA_TIMING_AGG && std::strcmp(name, "wta_hv") == 0;
+}
 
 // RAII helper: records timing events around one launch when enabled.
 struct ScopedKernelTimer {
@@ -79,8 +86,7 @@ struct ScopedKernelTimer {
     const char* name;
     hipEvent_t start = nullptr;
     ScopedKernelTimer(Ctx& ctx, const char* n) : c(ctx), name(n) {
-        if (c.timer.enabled && (!c.timer.paths_only || is_path_kernel(name)))
-            c.timer.begin(c.stream, name, &start);
+        if (timer_wants(c.timer, name)) c.timer.begin(c.stream, name, &start);
     }
     ~ScopedKernelTimer() {
         if (c.timer.enabled && start) c.timer.end(c.stream, name, start);
@@ -89,15 +95,16 @@ struct ScopedKernelTimer {
 
 // Timing of one launch through hipExtLaunchKernelGGL's start/stop events: the
 // runtime stamps them from the kernel's own dispatch, so no separate event
-// packets enter the stream (used for the path kernel, the one bench.py times
-// inside its timed region).  start/stop stay null when timing is off.
+// packets enter the stream (used for the two aggregation kernels, the ones
+// bench.py times inside its timed region).  start/stop stay null when timing
+// is off.
 struct DispatchTimer {
     Ctx& c;
     const char* name;
     hipEvent_t start = nullptr, stop = nullptr;
     bool used = false;   // set by the launch that received start/stop
     DispatchTimer(Ctx& ctx, const char* n) : c(ctx), name(n) {
-        if (c.timer.enabled && (!c.timer.paths_only || is_path_kernel(name))) {
+        if (timer_wants(c.timer, name)) {
             start = c.timer.get_event();
             stop = start ? c.timer.get_event() : nullptr;
             if (!stop && start) { c.timer.pool.push_back(start); start = nullptr; }

@@ -272,12 +272,18 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
                 // S(d*-1) and S(d*+1) through LDS: every lane writes its S
                 // pairs over the pixel's V block, which nothing reads again;
                 // as u16 the block is S indexed by d.  The owning lane reads
-                // the two neighbours (same wave: LDS keeps the order).
+                // the two neighbours (same wave, behind a wave barrier).
                 const unsigned best = wta_pick_key<DPL, PIN && tune::kWtahvPinWta>(S, k);
                 const int ds = (int)(best & 0xffffu);
                 if (want_sub) {
 #pragma unroll
                     for (int p = 0; p < NP; p++) vpix[k * NP + p] = S[p];
+                    // the owning lane reads what other lanes of this wave just
+                    // wrote: state the ordering (a wave's LDS operations
+                    // execute in issue order, so this costs no instruction)
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 }
                 if (k == j) {
                     dres = (unsigned)ds;
@@ -317,7 +323,7 @@ bool wta_hv_supported(int D) { return D == 64 || D == 128 || D == 192 || D == 25
 hipError_t launch_wta_hv(Ctx& c, const uint8_t* C, const uint8_t* L4, const uint8_t* CK,
                          const uint8_t* CKV, int W, int H, int D, int P1, int P2, int dmin,
                          uint16_t* disp, float* sub, int dreal) {
-    ScopedKernelTimer t(c, "wta_hv");
+    DispatchTimer t(c, "wta_hv");
     if (!wta_hv_supported(D)) return hipErrorInvalidValue;
     const TileGeom tg = tile_geom(W, H, D);
     WtaHvGeom g;
@@ -333,13 +339,14 @@ hipError_t launch_wta_hv(Ctx& c, const uint8_t* C, const uint8_t* L4, const uint
     g.vck = (unsigned)(tg.vck_bytes / 2);
     const bool pad = g.dreal < D;
     const dim3 grid((unsigned)(g.ntx * g.nty));
-#define SVA_WTAHV(DPL_, TYL_)                                                                  \
-    if (pad)                                                                                   \
-        hipLaunchKernelGGL((wta_hv_kernel<DPL_, TYL_, true>), grid, dim3(TB), 0, c.stream, C,  \
-                           L4, CK, CKV, g, disp, sub);                                         \
-    else                                                                                       \
-        hipLaunchKernelGGL((wta_hv_kernel<DPL_, TYL_, false>), grid, dim3(TB), 0, c.stream, C, \
-                           L4, CK, CKV, g, disp, sub)
+#define SVA_WTAHV(DPL_, TYL_)                                                                 \
+    if (pad)                                                                                  \
+        hipExtLaunchKernelGGL((wta_hv_kernel<DPL_, TYL_, true>), grid, dim3(TB), 0, c.stream, \
+                              t.start, t.stop, 0, C, L4, CK, CKV, g, disp, sub);              \
+    else                                                                                      \
+        hipExtLaunchKernelGGL((wta_hv_kernel<DPL_, TYL_, false>), grid, dim3(TB), 0,          \
+                              c.stream, t.start, t.stop, 0, C, L4, CK, CKV, g, disp, sub);    \
+    t.used = true
     constexpr int TYL = tune::kWtahvTileLog2, TYLW = tune::kWtahvTileLog2Wide;
     if (tg.seg_log2 != (D <= 128 ? TYL : TYLW)) return hipErrorInvalidValue;
     switch (D) {

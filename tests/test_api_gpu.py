@@ -138,8 +138,18 @@ def test_reserve_timing_and_errors(ctx, sva):
     assert ctx.kernel_time("sgm_paths")[1] == 2
     for name in ("census", "cost", "wta", "wta_h", "wta_hv"):
         assert ctx.kernel_time(name) == (0.0, 0), name
+    # SVA_TIMING_AGG: the two aggregation kernels (bench.py's aggregation roofline)
+    ctx.reset_timing()
+    ctx.set_timing(sva.SVA_TIMING_AGG)
+    ctx.disparity_sgm(L, R, sva.default_params(D=128))
+    ctx.set_timing(sva.SVA_TIMING_OFF)
+    for name in ("sgm_paths", "wta_hv"):
+        ms, n = ctx.kernel_time(name)
+        assert n == 1 and ms > 0.0, name
+    for name in ("census", "cost", "wta"):
+        assert ctx.kernel_time(name) == (0.0, 0), name
     with pytest.raises(sva.SvaError) as e:
-        ctx.set_timing(3)
+        ctx.set_timing(4)
     assert e.value.status == sva.SVA_ERR_INVALID_ARG
     assert ctx.kernel_time("no_such_kernel") == (0.0, 0)
     ctx.reset_timing()

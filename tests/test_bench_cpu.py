@@ -79,6 +79,29 @@ def test_live_success_uses_kernel_bytes(bench, monkeypatch):
     assert rf["traffic_per_kernel"] == kern
 
 
+def test_aggregation_roofline(bench, monkeypatch):
+    """sgm_paths + wta_hv graded together over SURVEY §8d's
+    aggregation (10 B/disp) + WTA (2 B/disp + 2 B/px) bytes; live PMC bytes
+    of both kernels fill its traffic."""
+    W, H, D = 1920, 1080, 128
+    kernels = {"sgm_paths": {"avg_ms": 0.5}, "wta_hv": {"avg_ms": 0.25}}
+    ag = bench.aggregation_roofline_of(kernels, W, H, D)
+    alg = 12.0 * W * H * D + 2.0 * W * H
+    assert ag["alg_bytes_per_launch"] == alg and ag["sum_ms"] == 0.75
+    assert abs(ag["achieved"] - alg / 0.75e-3 / 1e9) < 0.1
+    assert abs(ag["frac"] - ag["achieved"] / 8000.0) < 1e-4
+    assert bench.aggregation_roofline_of({"sgm_paths": {"avg_ms": 0.5}}, W, H, D) is None
+    monkeypatch.delenv("SVA_BENCH_PMC_CHILD", raising=False)
+    for k in [k for k in os.environ if k.startswith("ROCPROF")]:
+        monkeypatch.delenv(k)
+    kern = {"sgm_paths": {"hbm_bytes_per_launch": 3}, "wta_hv": {"hbm_bytes_per_launch": 4}}
+    monkeypatch.setattr(bench, "live_traffic", lambda a: kern)
+    out = line(bench)
+    out["aggregation_roofline"] = ag
+    bench.attach_traffic(args("live"), out, 1)
+    assert out["aggregation_roofline"]["traffic"] == 7
+
+
 def mode_args(**kw):
     d = dict(gpus=1, engine="auto", rehearse_rccl=False, rehearse_overlap=False,
              dist_backend="nccl")

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Stream-time cost of the bench's live kernel timing: ms per 1080p D=128
 frame for back-to-back frames with timing off (0), the roofline kernel's
-dispatch events only (2, what bench.py's timed region uses) and every
-kernel event-timed (1).  Modes alternate round by round on one context."""
+dispatch events only (2), both aggregation kernels' dispatch events (3, what
+bench.py's timed region uses) and every kernel event-timed (1).  Modes
+alternate round by round on one context."""
 import json
 import statistics
 import sys
@@ -42,11 +43,12 @@ def main():
         ctx.set_timing(0)
         return dt
 
-    for m in (0, 2, 1):
+    modes = (0, 2, 3, 1)
+    for m in modes:
         run(m)
-    res = {0: [], 2: [], 1: []}
+    res = {m: [] for m in modes}
     for _ in range(rounds):
-        for m in (0, 2, 1):
+        for m in modes:
             res[m].append(run(m))
     # one isolated frame (host sync before and after), as tools/ab_paths.py times them
     iso = []
