@@ -45,6 +45,10 @@ WORKLOADS = {
     # BASELINE configs[3] wording: an 8-camera array (2x4 grid), all 28 pairwise
     # baselines, fused per reference camera
     "grid8_all": dict(W=1920, H=1080, D=128, rig="grid8_all"),
+    # the reference's own frame size class: its renders are resized by 0.5
+    # before matching (CameraStereoVision.cpp:17-18), and SURVEY §6 measures
+    # D = 45-49 at 640 px; center8 at 960x540 D=64
+    "center8_half_d64": dict(W=960, H=540, D=64, rig="center8"),
     # BASELINE configs[4]: 256 synthetic 1080p pairs (seeds 0-255), D=192,
     # sharded over the ranks (32 per GPU at N=8): fixed total, strong scaling
     "batch256_d192": dict(W=1920, H=1080, D=192, total_pairs=256),
@@ -261,7 +265,7 @@ def committed_traffic(workload):
 
 
 # rocprofv3 kernel names -> bench timer names (the PMC pass reports per kernel)
-PMC_KERNELS = {"sgm_paths_kernel": "sgm_paths", "wta_h_kernel": "wta_h", "wta_hv_kernel": "wta_hv",
+PMC_KERNELS = {"sgm_paths_kernel": "sgm_paths", "wta_hv_kernel": "wta_hv",
                "census_cost_kernel": "cost"}
 
 
@@ -456,7 +460,7 @@ def exchange_report(a, step, world, rank, dev, ctxs, last, n_units, ms_per_step,
             "map_bytes_per_unit": int(last[0].numel() * last.element_size())}
 
 
-def kernel_table(ctx, names=("census", "cost", "sgm_paths", "wta_h", "wta_hv", "fuse_depth")):
+def kernel_table(ctx, names=("census", "cost", "sgm_paths", "wta_hv", "fuse_depth")):
     """Average hipEvent duration per kernel, pooled over one or several contexts
     (with --streams > 1 the launches overlap, so durations include contention)."""
     ctxs = ctx if isinstance(ctx, list) else [ctx]
@@ -683,6 +687,8 @@ def run_array(a, wl, world, rank, local, dev):
     elapsed = timed(a, step, world, dev, ctxs)
     kernels = breakdown(a, step, world, ctxs, kernel_table(ctxs))
     value = n_units * W * H * D * a.steps / elapsed / 1e6
+    # committed PMC bytes per pair: the 1080p D=128 frame's for the 1080p rigs
+    traffic_wl = "1080p_d128" if (W, H, D) == (1920, 1080, 128) else a.workload
     exchange = None
     if multi:
         def recompute(u):
@@ -737,9 +743,9 @@ def run_array(a, wl, world, rank, local, dev):
             "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
             "fused_maps_per_s": round(len(groups) * a.steps / elapsed, 2),
             "ref_interior_depth_exact_frac": round(exact, 4),
-            "roofline": roofline_of(kernels, W, H, D, "1080p_d128", overlapped=len(ctxs) > 1),
+            "roofline": roofline_of(kernels, W, H, D, traffic_wl, overlapped=len(ctxs) > 1),
             "aggregation_roofline": aggregation_roofline_of(kernels, W, H, D,
-                                                            committed_traffic("1080p_d128"),
+                                                            committed_traffic(traffic_wl),
                                                             overlapped=len(ctxs) > 1),
             "cpu_baseline": None,
         }

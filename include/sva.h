@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SVA_ABI_VERSION 4
+#define SVA_ABI_VERSION 5
 
 enum {
     SVA_OK = 0,
@@ -101,8 +101,10 @@ const char* sva_status_string(int status);
 int sva_reserve(void* ctx, int width, int height, int D);
 
 /* Path-aggregation route of sva_disparity_sgm*.  COST_VOLUME (= AUTO, the
- * default): census -> W*H*D u8 cost volume -> 8-path kernel in checkpoint
- * mode -> horizontal recompute + WTA.  FUSED (the
+ * default): census -> W*H*D u8 cost volume -> 8-path kernel writing the four
+ * diagonal volumes and the horizontal / vertical checkpoints -> per-tile
+ * recompute of those four directions + WTA (the tile pipeline, DESIGN.md
+ * §4.9).  FUSED (the
  * census-fused path kernel of ABI v1-v3, slower at every D once the
  * checkpoint route existed) was removed in ABI v4: selecting it returns
  * SVA_ERR_UNSUPPORTED. */
@@ -129,7 +131,11 @@ int sva_kernel_time(void* ctx, const char* name, double* total_ms, int64_t* coun
 /* ------------------------------------------------------ Mode S (SGM) --- */
 /* Whole path: census -> Hamming cost -> 8-path SGM -> WTA (+ sub-pixel).
  * Replaces the inline hot loop CameraStereoVision.cpp:44-95 with the
- * north_star SGM matcher.  disp: W*H u16 (dmin + d*); subpix: W*H f32 or NULL. */
+ * north_star SGM matcher.  disp: W*H u16 (dmin + d*); subpix: W*H f32 or NULL.
+ * Size limits (SVA_ERR_UNSUPPORTED beyond them): H <= 65535, and W*H*Dn < 2^32
+ * where Dn is D rounded up to 64, 128, 192 or 256 -- every volume is addressed
+ * with 32-bit byte offsets (e.g. 4K at D = 256 is 2.1e9, within the limit;
+ * 8K x 4K at D = 256 is not). */
 int sva_disparity_sgm(void* ctx, const uint8_t* left, const uint8_t* right, int width,
                       int height, size_t pitch, const sva_sgm_params* p, uint16_t* disp,
                       float* subpix);
@@ -139,7 +145,8 @@ int sva_disparity_sgm_d(void* ctx, const uint8_t* left, const uint8_t* right, in
 
 /* Stage entry points (device buffers).  Layouts: census W*H u64; C, L
  * [y][x][d] u8; S [y][x][d] u16; L volumes [8][y][x][d] (direction table in
- * DESIGN.md §2.3). */
+ * DESIGN.md §2.3).  Each buffer must hold exactly its documented shape for
+ * the (width, height, D) passed; the tile stages below take byte sizes. */
 int sva_census_d(void* ctx, const uint8_t* img, int width, int height, size_t pitch,
                  uint64_t* census);
 int sva_cost_d(void* ctx, const uint64_t* census_l, const uint64_t* census_r, int width,
@@ -153,18 +160,37 @@ int sva_paths_d(void* ctx, const uint8_t* C, int width, int height, const sva_sg
                 uint8_t* L8);
 int sva_aggregate_d(void* ctx, const uint8_t* C, int width, int height,
                     const sva_sgm_params* p, uint16_t* S);
-/* Checkpoint-mode stages of the cost-volume frame pipeline.
- * sva_paths_ckpt_d: L6 = [6][H][W][D] u8, the volumes of directions 2..7 (same
- * values as slots 2..7 of sva_paths_d); CK = [2][H][ns][D] u8, the horizontal
- * states: CK[0][y][s] = L_0(s*seg + seg - 1, y), CK[1][y][s] = L_1(s*seg, y)
- * (entries with no such column are not written).  sva_wta_h_d recomputes the
- * two horizontal directions per segment from CK and finishes S, WTA and the
- * sub-pixel map.  seg and ns from sva_ckpt_segments (no device needed). */
-int sva_ckpt_segments(int width, int D, int* ns, int* seg);
-int sva_paths_ckpt_d(void* ctx, const uint8_t* C, int width, int height, const sva_sgm_params* p,
-                     uint8_t* L6, uint8_t* CK);
-int sva_wta_h_d(void* ctx, const uint8_t* C, const uint8_t* L6, const uint8_t* CK, int width,
-                int height, const sva_sgm_params* p, uint16_t* disp, float* subpix);
+/* The two stages of the frame route, the tile pipeline.
+ *   sva_paths_tile_d: diag = [4][H][W][D] u8, the volumes of directions 4..7
+ *     (slot r - 4; same values as slots 4..7 of sva_paths_d); hckpt =
+ *     [2][H][nsx][D] u8, hckpt[0][y][s] = L_0(s*seg + seg - 1, y) and
+ *     hckpt[1][y][s] = L_1(s*seg, y); vckpt = [2][nsy][W][D] u8, vckpt[0][s][x]
+ *     = L_2(x, s*seg + seg - 1) and vckpt[1][s][x] = L_3(x, s*seg) (entries
+ *     with no such column / row are not written).
+ *   sva_wta_hv_d: recomputes directions 0..3 per 16 x seg tile from the
+ *     checkpoints, sums S with the diagonal volumes, picks d* (+ sub-pixel).
+ * Every buffer comes with its size in bytes: a buffer smaller than its plane
+ * returns SVA_ERR_INVALID_ARG before anything is launched.  seg, nsx, nsy and
+ * the plane sizes come from sva_tile_layout_of (no device needed);
+ * sva_tile_check applies the entry points' size test alone. */
+typedef struct sva_tile_layout {
+    int32_t seg;          /* checkpoint spacing, columns and rows            */
+    int32_t nsx, nsy;     /* ceil(W / seg), ceil(H / seg)                    */
+    size_t cost_bytes;    /* C      [H][W][D]                                */
+    size_t diag_bytes;    /* diag   [4][H][W][D]                             */
+    size_t hckpt_bytes;   /* hckpt  [2][H][nsx][D]                           */
+    size_t vckpt_bytes;   /* vckpt  [2][nsy][W][D]                           */
+} sva_tile_layout;
+int sva_tile_layout_of(int width, int height, int D, sva_tile_layout* out);
+int sva_tile_check(int width, int height, int D, size_t C_bytes, size_t diag_bytes,
+                   size_t hckpt_bytes, size_t vckpt_bytes);
+int sva_paths_tile_d(void* ctx, const uint8_t* C, size_t C_bytes, int width, int height,
+                     const sva_sgm_params* p, uint8_t* diag, size_t diag_bytes, uint8_t* hckpt,
+                     size_t hckpt_bytes, uint8_t* vckpt, size_t vckpt_bytes);
+int sva_wta_hv_d(void* ctx, const uint8_t* C, size_t C_bytes, const uint8_t* diag,
+                 size_t diag_bytes, const uint8_t* hckpt, size_t hckpt_bytes,
+                 const uint8_t* vckpt, size_t vckpt_bytes, int width, int height,
+                 const sva_sgm_params* p, uint16_t* disp, float* subpix);
 int sva_wta_d(void* ctx, const uint16_t* S, int width, int height, const sva_sgm_params* p,
               uint16_t* disp, float* subpix);
 

@@ -35,7 +35,7 @@ SVA_TIMING_ALL = 1
 SVA_TIMING_PATHS = 2
 SVA_TIMING_AGG = 3
 # The ABI this binding is written against (include/sva.h SVA_ABI_VERSION).
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # Symbols declared in include/sva.h (checked by tests/test_abi.py).
 EXPORTED = [
@@ -51,8 +51,8 @@ EXPORTED = [
     "sva_points_to_depth_d", "sva_points_to_depth", "sva_depth_to_points_d",
     "sva_depth_to_points", "sva_resize_half_size", "sva_resize_half_d", "sva_resize_half",
     "sva_batch_sgm", "sva_resize_linear_f64_d", "sva_resize_linear_f64", "sva_ref_error_d",
-    "sva_ref_error", "sva_masked_mean_d", "sva_masked_mean", "sva_ckpt_segments",
-    "sva_paths_ckpt_d", "sva_wta_h_d", "sva_multi_create", "sva_multi_destroy",
+    "sva_ref_error", "sva_masked_mean_d", "sva_masked_mean", "sva_tile_layout_of",
+    "sva_tile_check", "sva_paths_tile_d", "sva_wta_hv_d", "sva_multi_create", "sva_multi_destroy",
     "sva_multi_synchronize", "sva_multi_last_error", "sva_multi_plan", "sva_multi_context",
     "sva_batch_sgm_d", "sva_array_depth",
 ]
@@ -82,6 +82,13 @@ class Camera(ct.Structure):
         c.pos[0], c.pos[1], c.pos[2] = pos
         c.pixel_size = pixel_size
         return c
+
+
+class TileLayout(ct.Structure):
+    """Mirror of ``sva_tile_layout`` (include/sva.h): the tile stages' buffers."""
+    _fields_ = [("seg", ct.c_int32), ("nsx", ct.c_int32), ("nsy", ct.c_int32),
+                ("cost_bytes", ct.c_size_t), ("diag_bytes", ct.c_size_t),
+                ("hckpt_bytes", ct.c_size_t), ("vckpt_bytes", ct.c_size_t)]
 
 
 class PairJob(ct.Structure):
@@ -156,9 +163,11 @@ def _load() -> ct.CDLL:
         "sva_census_cost_d": (i32, [vp, vp, vp, i32, i32, sz, P(SgmParams), vp]),
         "sva_aggregate_d": (i32, [vp, vp, i32, i32, P(SgmParams), vp]),
         "sva_wta_d": (i32, [vp, vp, i32, i32, P(SgmParams), vp, vp]),
-        "sva_ckpt_segments": (i32, [i32, i32, P(i32), P(i32)]),
-        "sva_paths_ckpt_d": (i32, [vp, vp, i32, i32, P(SgmParams), vp, vp]),
-        "sva_wta_h_d": (i32, [vp, vp, vp, vp, i32, i32, P(SgmParams), vp, vp]),
+        "sva_tile_layout_of": (i32, [i32, i32, i32, P(TileLayout)]),
+        "sva_tile_check": (i32, [i32, i32, i32, sz, sz, sz, sz]),
+        "sva_paths_tile_d": (i32, [vp, vp, sz, i32, i32, P(SgmParams), vp, sz, vp, sz, vp, sz]),
+        "sva_wta_hv_d": (i32, [vp, vp, sz, vp, sz, vp, sz, vp, sz, i32, i32, P(SgmParams), vp,
+                               vp]),
         "sva_disparity_ref": (i32, [vp, vp, vp, i32, i32, sz, vp, P(Camera), P(Camera), i32,
                                     dbl, dbl, vp, vp, vp]),
         "sva_disparity_ref_d": (i32, [vp, vp, vp, i32, i32, sz, vp, P(Camera), P(Camera), i32,
@@ -231,13 +240,13 @@ def resize_half_size(W: int, H: int):
     return dw.value, dh.value
 
 
-def ckpt_segments(W: int, D: int):
-    """(ns, seg) of the horizontal checkpoint layout (sva_ckpt_segments)."""
-    ns, seg = ct.c_int(), ct.c_int()
-    st = lib.sva_ckpt_segments(W, D, ct.byref(ns), ct.byref(seg))
-    if st:
-        raise SvaError(st, "sva_ckpt_segments")
-    return ns.value, seg.value
+def tile_layout(W: int, H: int, D: int) -> TileLayout:
+    """Plane sizes of the tile stages (sva_tile_layout_of; no device needed)."""
+    out = TileLayout()
+    st = lib.sva_tile_layout_of(W, H, D, ct.byref(out))
+    if st != SVA_OK:
+        raise SvaError(st, "sva_tile_layout_of")
+    return out
 
 
 def device_count() -> int:
@@ -359,12 +368,17 @@ class Context:
     def aggregate_d(self, C, W, H, params, S):
         self._chk(lib.sva_aggregate_d(self.h, _ptr(C), W, H, ct.byref(params), _ptr(S)))
 
-    def paths_ckpt_d(self, C, W, H, params, L6, CK):
-        self._chk(lib.sva_paths_ckpt_d(self.h, _ptr(C), W, H, ct.byref(params), _ptr(L6), _ptr(CK)))
+    def paths_tile_d(self, C, C_bytes, W, H, params, diag, diag_bytes, hck, hck_bytes, vck,
+                     vck_bytes):
+        self._chk(lib.sva_paths_tile_d(self.h, _ptr(C), C_bytes, W, H, ct.byref(params),
+                                       _ptr(diag), diag_bytes, _ptr(hck), hck_bytes, _ptr(vck),
+                                       vck_bytes))
 
-    def wta_h_d(self, C, L6, CK, W, H, params, disp, sub=None):
-        self._chk(lib.sva_wta_h_d(self.h, _ptr(C), _ptr(L6), _ptr(CK), W, H, ct.byref(params),
-                                  _ptr(disp), _ptr(sub)))
+    def wta_hv_d(self, C, C_bytes, diag, diag_bytes, hck, hck_bytes, vck, vck_bytes, W, H, params,
+                 disp, sub=None):
+        self._chk(lib.sva_wta_hv_d(self.h, _ptr(C), C_bytes, _ptr(diag), diag_bytes, _ptr(hck),
+                                   hck_bytes, _ptr(vck), vck_bytes, W, H, ct.byref(params),
+                                   _ptr(disp), _ptr(sub)))
 
     def wta_d(self, S, W, H, params, disp, sub=None):
         self._chk(lib.sva_wta_d(self.h, _ptr(S), W, H, ct.byref(params), _ptr(disp), _ptr(sub)))

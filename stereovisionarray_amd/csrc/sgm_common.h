@@ -1,6 +1,6 @@
 // sgm_common.h -- device pieces of the 8-path aggregation shared by the path
-// kernel (sgm_paths.hip) and the horizontal recompute + WTA kernel
-// (wta_h.hip).  DESIGN.md §4.3 / §4.6.
+// kernel (sgm_paths.hip) and the tile recompute + WTA kernel (wta_hv.hip).
+// DESIGN.md §4.3 / §4.9.
 #pragma once
 
 #include <utility>
@@ -31,24 +31,21 @@ struct PathGeom {
     int blk_h;    // blocks per horizontal direction (H lines)
     int blk_w;    // blocks per vertical / diagonal direction (W lines)
     size_t vol;   // bytes of one direction volume (W*H*D)
-    int ckpt;     // 1: horizontal lines store only segment checkpoints (below);
-                  // 2: vertical lines too (tile pipeline, wta_hv.hip)
-    int ns;       // checkpoint segments per row, ceil(W / seg)
-    size_t ckvol; // bytes of one direction's checkpoint plane (H*ns*D)
-    int nsy;      // ckpt 2: vertical checkpoint segments per column, ceil(H / seg)
-    size_t ckvvol; // ckpt 2: bytes of one vertical checkpoint plane (nsy*W*D)
+    int ckpt;     // 2: the tile pipeline's checkpoints (below); 0: eight volumes
+    int ns;       // horizontal checkpoint segments per row, ceil(W / seg)
+    size_t ckvol; // bytes of one horizontal checkpoint plane (H*ns*D)
+    int nsy;      // vertical checkpoint segments per column, ceil(H / seg)
+    size_t ckvvol; // bytes of one vertical checkpoint plane (nsy*W*D)
 };
 
-// Horizontal-line checkpoints.  With g.ckpt set, the two
-// horizontal directions write no L_r volume: direction 0 (left to right)
-// stores L(x) at the last column of every seg-wide segment but the row's
-// last, direction 1 (right to left) at the first column of every segment but
-// the first; [2][H][ns][D] u8.  The WTA kernel (wta_h.hip) re-runs both
-// recurrences segment by segment from these states, so their L_r bytes never
-// reach HBM.  seg = 32 columns up to D = 128 and 16 above: wta_h keeps a
-// segment's left-to-right L in registers, seg * D/64 dwords per lane.
-template <int DPL> constexpr int seg_log2() { return DPL <= 8 ? 5 : 4; }
-inline int seg_log2_of(int D) { return D <= 128 ? 5 : 4; }
+// Tile-pipeline checkpoints.  With g.ckpt set, the
+// horizontal and vertical directions write no L_r volume: direction 0 (left
+// to right) stores L(x) at the last column of every seg-wide segment but the
+// row's last, direction 1 (right to left) at the first column of every
+// segment but the first ([2][H][ns][D] u8), and the vertical directions the
+// same along their columns ([2][nsy][W][D] u8).  wta_hv.hip re-runs all four
+// recurrences tile by tile from these states, so their L_r bytes never reach
+// HBM.
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
@@ -408,7 +405,7 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
 }
 
 
-// ---- shared by the final kernels (wta_h.hip, wta_hv.hip) ------------------
+// ---- shared by the final kernels (wta.hip, wta_hv.hip) ---------------------
 
 template <int NW>
 __device__ __forceinline__ void unpack_add(const unsigned (&w)[NW], unsigned (&S)[2 * NW]) {

@@ -27,15 +27,14 @@
 // Two output modes (g.ckpt):
 //   0  every direction writes its u8 volume, [8][H][W][D] (sva_paths_d, the
 //      stage API the parity tests read): 8 C reads + 8 L writes per disparity.
-//   1  the frame pipeline: the vertical and diagonal
-//      directions write [6][H][W][D] (direction r at slot r - 2); the two
-//      horizontal ones store only segment checkpoints, [2][H][ns][D], and
-//      wta_h.hip recomputes them per segment: 8 C reads + 6 L writes.
-//   2  the tile pipeline: only the four diagonal directions
-//      write volumes, [4][H][W][D] (direction r at slot r - 4); horizontal
-//      lines store checkpoints every seg columns, vertical lines every seg
-//      rows ([2][nsy][W][D]; seg = 2^tile_geom().seg_log2), and wta_hv.hip
-//      recomputes all four per tile: 8 C reads + 4 L writes.
+//   2  the frame route, the tile pipeline: only the four
+//      diagonal directions write volumes, [4][H][W][D] (direction r at slot
+//      r - 4); horizontal lines store checkpoints every seg columns
+//      ([2][H][nsx][D]), vertical lines every seg rows ([2][nsy][W][D]; seg =
+//      2^tile_geom().seg_log2), and wta_hv.hip recomputes all four per tile:
+//      8 C reads + 4 L writes.
+//   (Mode 1, the round-2 route of DESIGN.md §4.6 -- six volumes, horizontal
+//   checkpoints only, finished by wta_h.hip -- was removed in ABI v5.)
 #include "sgm_common.h"
 #include "sva_tuning.h"
 
@@ -80,25 +79,21 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
     int rx, ry;
     dir_of(r, rx, ry);
     const rsrc_t rC = make_rsrc(C, g.vol);
-    const int slot = g.ckpt == 2 ? r - 4 : g.ckpt ? r - 2 : r;
-    // checkpoint segments: the §4.6 route's, or the tile pipeline's (§4.9)
-    constexpr int SL1 = seg_log2<DPL>();
-    constexpr int SL2 = DPL <= 8 ? tune::kWtahvTileLog2 : tune::kWtahvTileLog2Wide;
+    const int slot = g.ckpt ? r - 4 : r;
+    // the tile pipeline's checkpoint segment (§4.9), rows and columns
+    constexpr int SL = DPL <= 8 ? tune::kWtahvTileLog2 : tune::kWtahvTileLog2Wide;
     if (r >= 4) {
         const rsrc_t rL = make_rsrc(L8 + (size_t)slot * g.vol, g.vol);
         path_line<DPL, true, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
-    } else if (r >= 2 && g.ckpt == 2) {
+    } else if (r >= 2 && g.ckpt) {
         const rsrc_t rCK = make_rsrc(CKV + (size_t)(r - 2) * g.ckvvol, g.ckvvol);
-        path_line<DPL, false, pf_v<DPL>(), 2, SL2>(rC, rC, g, rx, ry, line, k, rCK);
+        path_line<DPL, false, pf_v<DPL>(), 2, SL>(rC, rC, g, rx, ry, line, k, rCK);
     } else if (r >= 2) {
         const rsrc_t rL = make_rsrc(L8 + (size_t)slot * g.vol, g.vol);
         path_line<DPL, false, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
     } else if (g.ckpt) {
         const rsrc_t rCK = make_rsrc(CK + (size_t)r * g.ckvol, g.ckvol);
-        if (g.ckpt == 2)
-            path_line<DPL, false, pf_h<DPL>(), 1, SL2>(rC, rC, g, rx, ry, line, k, rCK);
-        else
-            path_line<DPL, false, pf_h<DPL>(), 1, SL1>(rC, rC, g, rx, ry, line, k, rCK);
+        path_line<DPL, false, pf_h<DPL>(), 1, SL>(rC, rC, g, rx, ry, line, k, rCK);
     } else {
         const rsrc_t rL = make_rsrc(L8 + (size_t)r * g.vol, g.vol);
         path_line<DPL, false, pf_h<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
@@ -108,10 +103,6 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
 }  // namespace
 
 bool paths_supported(int D) { return D == 64 || D == 128 || D == 192 || D == 256; }
-
-int sgm_seg_log2(int D) { return seg_log2_of(D); }
-
-int ckpt_segments(int W, int D) { return (W + (1 << seg_log2_of(D)) - 1) >> seg_log2_of(D); }
 
 TileGeom tile_geom(int W, int H, int D) {
     TileGeom t;
@@ -133,19 +124,13 @@ hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, i
     g.blk_h = (H + LINES_PER_BLOCK - 1) / LINES_PER_BLOCK;
     g.blk_w = (W + LINES_PER_BLOCK - 1) / LINES_PER_BLOCK;
     g.vol = (size_t)W * H * D;
-    g.ckpt = CKV ? 2 : CK ? 1 : 0;
-    int hsl = seg_log2_of(D);            // the kernel's SL1 / SL2 for this D
-    g.nsy = 0;
-    g.ckvvol = 0;
-    if (CKV) {
-        if (!CK) return hipErrorInvalidValue;
-        const TileGeom tg = tile_geom(W, H, D);
-        hsl = tg.seg_log2;
-        g.nsy = tg.nty;
-        g.ckvvol = tg.vck_bytes / 2;
-    }
-    g.ns = (W + (1 << hsl) - 1) >> hsl;
-    g.ckvol = (size_t)H * g.ns * D;
+    if ((CK == nullptr) != (CKV == nullptr)) return hipErrorInvalidValue;
+    g.ckpt = CK ? 2 : 0;
+    const TileGeom tg = tile_geom(W, H, D);
+    g.nsy = tg.nty;
+    g.ckvvol = tg.vck_bytes / 2;
+    g.ns = tg.nsx;
+    g.ckvol = tg.hck_bytes / 2;
     if (g.vol >= (size_t)1 << 32) return hipErrorInvalidValue;  // 32-bit buffer offsets
     dim3 grid(2 * g.blk_h + 6 * g.blk_w);
 #define SVA_PATHS_LAUNCH(DPL_)                                                               \

@@ -166,44 +166,58 @@ int check_sgm(Ctx* c, const sva_sgm_params* p, int W, int H, bool native = false
     return SVA_OK;
 }
 
-// The frame route: the tile pipeline (§4.9) at every native D; it was the
-// faster route at every frame size measured, 640x480 D=64 included.
-bool use_tiles(int W, int H, int Dp) {
-    (void)W; (void)H;
-    return wta_hv_supported(Dp);
-}
-
-size_t ckpt_bytes(int W, int H, int D) { return 2 * (size_t)H * ckpt_segments(W, D) * (size_t)D; }
-
-// Paths + WTA of the cost-volume frame pipeline: sgm_paths
-// in checkpoint mode (6 volumes + horizontal checkpoints), then wta_h, which
-// recomputes the two horizontal directions per segment and picks d*.  Dp is
-// the native volume width, p->D <= Dp the caller's disparities (§4.7).
+// Paths + WTA of the frame pipeline, the tile pipeline: the
+// path kernel writes the four diagonal volumes plus horizontal and vertical
+// checkpoints, and wta_hv recomputes the other four directions per tile and
+// picks d*.  Dp is the native volume width, p->D <= Dp the caller's
+// disparities (§4.7).  (The round-2 route of §4.6 -- six volumes, finished
+// by wta_h -- was slower at every frame size measured and left in ABI v5.)
 int paths_wta(Ctx* c, const uint8_t* C, int W, int H, const sva_sgm_params* p, int Dp,
               uint16_t* disp, float* sub) {
+    if (!wta_hv_supported(Dp)) return fail(c, SVA_ERR_UNSUPPORTED, "no tile pipeline for this D");
     const size_t nv = (size_t)W * H * (size_t)Dp;
-    if (use_tiles(W, H, Dp)) {
-        // tile pipeline: four diagonal volumes + horizontal
-        // and vertical checkpoints, recomputed per tile by wta_hv
-        const TileGeom tg = tile_geom(W, H, Dp);
-        SVA_HIP(c, c->paths.ensure(nv * 4), "path workspace");
-        SVA_HIP(c, c->ckpt.ensure(tg.hck_bytes + tg.vck_bytes), "checkpoint workspace");
-        uint8_t* L4 = (uint8_t*)c->paths.ptr;
-        uint8_t* CK = (uint8_t*)c->ckpt.ptr;
-        uint8_t* CKV = CK + tg.hck_bytes;
-        SVA_HIP(c, launch_paths(*c, C, W, H, Dp, p->P1, p->P2, L4, CK, CKV), "paths launch");
-        SVA_HIP(c, launch_wta_hv(*c, C, L4, CK, CKV, W, H, Dp, p->P1, p->P2, p->dmin, disp, sub,
-                                 p->D),
-                "wta launch");
-        return SVA_OK;
-    }
-    SVA_HIP(c, c->paths.ensure(nv * 6), "path workspace");
-    SVA_HIP(c, c->ckpt.ensure(ckpt_bytes(W, H, Dp)), "checkpoint workspace");
-    uint8_t* L6 = (uint8_t*)c->paths.ptr;
+    const TileGeom tg = tile_geom(W, H, Dp);
+    SVA_HIP(c, c->paths.ensure(nv * 4), "path workspace");
+    SVA_HIP(c, c->ckpt.ensure(tg.hck_bytes + tg.vck_bytes), "checkpoint workspace");
+    uint8_t* L4 = (uint8_t*)c->paths.ptr;
     uint8_t* CK = (uint8_t*)c->ckpt.ptr;
-    SVA_HIP(c, launch_paths(*c, C, W, H, Dp, p->P1, p->P2, L6, CK), "paths launch");
-    SVA_HIP(c, launch_wta_h(*c, C, L6, CK, W, H, Dp, p->P1, p->P2, p->dmin, disp, sub, p->D),
+    uint8_t* CKV = CK + tg.hck_bytes;
+    SVA_HIP(c, launch_paths(*c, C, W, H, Dp, p->P1, p->P2, L4, CK, CKV), "paths launch");
+    SVA_HIP(c, launch_wta_hv(*c, C, L4, CK, CKV, W, H, Dp, p->P1, p->P2, p->dmin, disp, sub, p->D),
             "wta launch");
+    return SVA_OK;
+}
+
+// Buffer sizes of the tile-pipeline stages (sva_tile_layout).
+sva_tile_layout tile_layout(int W, int H, int D) {
+    sva_tile_layout l;
+    std::memset(&l, 0, sizeof(l));
+    const TileGeom tg = tile_geom(W, H, D);
+    l.seg = 1 << tg.seg_log2;
+    l.nsx = tg.nsx;
+    l.nsy = tg.nty;
+    l.cost_bytes = (size_t)W * H * (size_t)D;
+    l.diag_bytes = 4 * l.cost_bytes;
+    l.hckpt_bytes = tg.hck_bytes;
+    l.vckpt_bytes = tg.vck_bytes;
+    return l;
+}
+
+// Caller buffers of the tile stages against the layout: every buffer present
+// and at least as large as its plane, so that a sizing slip is an argument
+// error before anything reaches the device.
+int check_tile_buffers(Ctx* c, int W, int H, int D, const void* C, size_t C_bytes,
+                       const void* diag, size_t diag_bytes, const void* hck, size_t hck_bytes,
+                       const void* vck, size_t vck_bytes) {
+    const sva_tile_layout l = tile_layout(W, H, D);
+    if (!C || !diag || !hck || !vck) return fail(c, SVA_ERR_INVALID_ARG, "null stage buffer");
+    if (C_bytes < l.cost_bytes) return fail(c, SVA_ERR_INVALID_ARG, "cost buffer smaller than [H][W][D]");
+    if (diag_bytes < l.diag_bytes)
+        return fail(c, SVA_ERR_INVALID_ARG, "diagonal volume buffer smaller than [4][H][W][D]");
+    if (hck_bytes < l.hckpt_bytes)
+        return fail(c, SVA_ERR_INVALID_ARG, "horizontal checkpoint buffer smaller than [2][H][nsx][D]");
+    if (vck_bytes < l.vckpt_bytes)
+        return fail(c, SVA_ERR_INVALID_ARG, "vertical checkpoint buffer smaller than [2][nsy][W][D]");
     return SVA_OK;
 }
 
@@ -449,14 +463,10 @@ int sva_reserve(void* ctx, int W, int H, int D) {
     SVA_HIP(c, c->census_l.ensure(np * 8), "reserve");
     SVA_HIP(c, c->census_r.ensure(np * 8), "reserve");
     SVA_HIP(c, c->cost.ensure(nv), "reserve");
-    // the frame route's path volumes: 4 diagonal directions (tile pipeline)
-    SVA_HIP(c, c->paths.ensure(nv * (use_tiles(W, H, D) ? 4 : 6)), "reserve");
-    size_t ck = ckpt_bytes(W, H, D);                  // stage API / wta_h route
-    if (use_tiles(W, H, D)) {                         // the tile pipeline's frames
-        const TileGeom tg = tile_geom(W, H, D);
-        ck = std::max(ck, tg.hck_bytes + tg.vck_bytes);
-    }
-    SVA_HIP(c, c->ckpt.ensure(ck), "reserve");
+    // the frame route's path volumes: the 4 diagonal directions (tile pipeline)
+    SVA_HIP(c, c->paths.ensure(nv * 4), "reserve");
+    const TileGeom tg = tile_geom(W, H, D);
+    SVA_HIP(c, c->ckpt.ensure(tg.hck_bytes + tg.vck_bytes), "reserve");
     return SVA_OK;
 }
 
@@ -608,34 +618,48 @@ int sva_aggregate_d(void* ctx, const uint8_t* C, int W, int H, const sva_sgm_par
     return SVA_OK;
 }
 
-int sva_ckpt_segments(int W, int D, int* ns, int* seg) {
-    if (W <= 0 || !paths_supported(D) || !ns || !seg) return SVA_ERR_INVALID_ARG;
-    *ns = ckpt_segments(W, D);
-    *seg = 1 << sgm_seg_log2(D);
+int sva_tile_layout_of(int W, int H, int D, sva_tile_layout* out) {
+    if (!out || W <= 0 || H <= 0 || !paths_supported(D)) return SVA_ERR_INVALID_ARG;
+    *out = tile_layout(W, H, D);
     return SVA_OK;
 }
 
-int sva_paths_ckpt_d(void* ctx, const uint8_t* C, int W, int H, const sva_sgm_params* p,
-                     uint8_t* L6, uint8_t* CK) {
+int sva_tile_check(int W, int H, int D, size_t C_bytes, size_t diag_bytes, size_t hckpt_bytes,
+                   size_t vckpt_bytes) {
+    if (W <= 0 || H <= 0 || !paths_supported(D)) return SVA_ERR_INVALID_ARG;
+    const char one = 0;   // any non-null address: sizes only
+    return check_tile_buffers(nullptr, W, H, D, &one, C_bytes, &one, diag_bytes, &one, hckpt_bytes,
+                              &one, vckpt_bytes);
+}
+
+int sva_paths_tile_d(void* ctx, const uint8_t* C, size_t C_bytes, int W, int H,
+                     const sva_sgm_params* p, uint8_t* diag, size_t diag_bytes, uint8_t* hckpt,
+                     size_t hckpt_bytes, uint8_t* vckpt, size_t vckpt_bytes) {
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
     if ((s = check_sgm(c, p, W, H, true))) return s;
-    if (!C || !L6 || !CK || W <= 0 || H <= 0) return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
-    SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, L6, CK), "paths launch");
+    if ((s = check_tile_buffers(c, W, H, p->D, C, C_bytes, diag, diag_bytes, hckpt, hckpt_bytes,
+                                vckpt, vckpt_bytes)))
+        return s;
+    SVA_HIP(c, launch_paths(*c, C, W, H, p->D, p->P1, p->P2, diag, hckpt, vckpt), "paths launch");
     return SVA_OK;
 }
 
-int sva_wta_h_d(void* ctx, const uint8_t* C, const uint8_t* L6, const uint8_t* CK, int W, int H,
-                const sva_sgm_params* p, uint16_t* disp, float* sub) {
+int sva_wta_hv_d(void* ctx, const uint8_t* C, size_t C_bytes, const uint8_t* diag,
+                 size_t diag_bytes, const uint8_t* hckpt, size_t hckpt_bytes, const uint8_t* vckpt,
+                 size_t vckpt_bytes, int W, int H, const sva_sgm_params* p, uint16_t* disp,
+                 float* sub) {
     Ctx* c = as_ctx(ctx);
     SVA_CHECK_CTX(c);
     int s;
     if ((s = check_sgm(c, p, W, H, true))) return s;
-    if (!C || !L6 || !CK || !disp || W <= 0 || H <= 0)
-        return fail(c, SVA_ERR_INVALID_ARG, "bad argument");
-    SVA_HIP(c, launch_wta_h(*c, C, L6, CK, W, H, p->D, p->P1, p->P2, p->dmin, disp,
-                            p->subpixel ? sub : nullptr),
+    if ((s = check_tile_buffers(c, W, H, p->D, C, C_bytes, diag, diag_bytes, hckpt, hckpt_bytes,
+                                vckpt, vckpt_bytes)))
+        return s;
+    if (!disp) return fail(c, SVA_ERR_INVALID_ARG, "null disparity output");
+    SVA_HIP(c, launch_wta_hv(*c, C, diag, hckpt, vckpt, W, H, p->D, p->P1, p->P2, p->dmin, disp,
+                             p->subpixel ? sub : nullptr),
             "wta launch");
     return SVA_OK;
 }

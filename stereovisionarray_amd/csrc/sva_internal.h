@@ -136,11 +136,10 @@ hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right,
                               size_t pitch, int D, int dmin, int dir, uint8_t* C, int dreal = 0);
 hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,
                        int dmin, int dir, uint8_t* C, int dreal = 0);
-// sgm_paths.hip -- all 8 directions in one launch.  CK == nullptr: L8 =
-// [8][H][W][D] u8.  CK set (checkpoint mode): L8 = [6][H][W][D]
-// (directions 2..7) and CK = [2][H][ckpt_segments(W, D)][D] horizontal states.
-// CKV set as well (tile mode): L8 = [4][H][W][D] (directions
-// 4..7), CK = [2][H][nsx][D] and CKV = [2][nsy][W][D] (tile_geom below).
+// sgm_paths.hip -- all 8 directions in one launch.  CK == CKV == nullptr:
+// L8 = [8][H][W][D] u8.  CK and CKV set (the tile pipeline):
+// L8 = [4][H][W][D] (directions 4..7), CK = [2][H][nsx][D] and CKV =
+// [2][nsy][W][D] (tile_geom below).
 hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
                         uint8_t* L8, uint8_t* CK = nullptr, uint8_t* CKV = nullptr);
 // Tile pipeline geometry: tiles of 16 columns x seg rows (seg = 2^seg_log2),
@@ -160,16 +159,10 @@ bool paths_supported(int D);
 inline int padded_D(int D) {
     return D <= 0 ? 0 : D <= 64 ? 64 : D <= 128 ? 128 : D <= 192 ? 192 : D <= 256 ? 256 : 0;
 }
-int ckpt_segments(int W, int D);
-int sgm_seg_log2(int D);
-// wta_h.hip -- horizontal recompute from the checkpoints + sum + WTA.
-// dreal < D: a padded frame, WTA over d < dreal only.
-hipError_t launch_wta_h(Ctx& c, const uint8_t* C, const uint8_t* L6, const uint8_t* CK, int W,
-                        int H, int D, int P1, int P2, int dmin, uint16_t* disp, float* sub,
-                        int dreal = 0);
 // wta_hv.hip -- the tile pipeline's final kernel: horizontal + vertical
 // recompute from the checkpoints of launch_paths(.., CK, CKV), sum with the
-// four diagonal volumes L4, WTA.
+// four diagonal volumes L4, WTA.  dreal < D: a padded frame (DESIGN.md
+// §4.7), WTA over d < dreal only.
 bool wta_hv_supported(int D);
 hipError_t launch_wta_hv(Ctx& c, const uint8_t* C, const uint8_t* L4, const uint8_t* CK,
                          const uint8_t* CKV, int W, int H, int D, int P1, int P2, int dmin,

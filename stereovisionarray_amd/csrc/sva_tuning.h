@@ -29,8 +29,8 @@ constexpr int kPfH16 = 12, kPfV16 = 8;
 // Cache-policy bits of the cost-volume loads.  A/B (full frame, in-process):
 // nt (2) +8 %, sc0+nt (3) +8 %; sc0 (1), sc0+sc1 (17), 8, 16 within noise.
 constexpr int kCLoadAux = 0;
-// Cache-policy bits of the horizontal checkpoint stores (0 = default: wta_h
-// reads them back soon).  nt (2) measured: frame 0.952 vs 0.963 ms median,
+// Cache-policy bits of the checkpoint stores (0 = default: wta_hv reads them
+// back soon).  nt (2) measured: frame 0.952 vs 0.963 ms median,
 // min 0.948 vs 0.942 -- noise (profiles/r03_v6/ab_retune_sgm.log.txt).
 constexpr int kCkptStoreAux = 0;
 
@@ -40,17 +40,6 @@ constexpr int kCkptStoreAux = 0;
 // within 1 % either way, never slower beyond noise
 // (profiles/r03_v8/ab_state_min_tree.log.txt).
 constexpr int kStateMinTree = 1;
-
-// ---- wta_h.hip --------------------------------------------
-// Prefetch depth (steps) of the forward pass (1 cost load per step) and the
-// backward pass (6 volume loads per step); D > 128 halves the forward ring
-// and keeps 4 for the backward one (4 beats 2 and 3: 1080p D=192 -2 %, 4K
-// D=256 -2.4 %; deeper at D=128, 6 or 8, within noise).
-constexpr int kWtahPfFwd = 8, kWtahPfBwd = 4;
-constexpr int kWtahPfFwdWide = 4, kWtahPfBwdWide = 4;
-// Pixels of a segment whose cost words wta_h keeps in LDS for the backward
-// pass (0 = the whole segment); the others are re-read from global memory.
-constexpr int kWtahLdsPix = 0;
 
 // ---- wta_hv.hip -------------------------------------------
 // log2 of the tile rows and of the checkpoint segment (tiles are 16 x 2^this).

@@ -5,7 +5,7 @@
 // holds disparities [k*DPL, k*DPL+DPL).  S = sum of the 8 u8 path volumes is
 // formed in packed u16 (no carry: S <= 8*255 < 2^16); the pick is
 // wta_common.h's.  These kernels serve the stage API (sva_wta_d,
-// sva_aggregate_d); the frame pipeline uses wta_h.hip, which also recomputes
+// sva_aggregate_d); the frame pipeline uses wta_hv.hip, which also recomputes
 // the horizontal paths.
 #include "sva_device.h"
 #include "sva_internal.h"

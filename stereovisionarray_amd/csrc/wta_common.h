@@ -1,5 +1,5 @@
 // wta_common.h -- first-minimum WTA + parabola sub-pixel on one 16-lane DPP
-// row, shared by wta.hip and wta_h.hip.
+// row, shared by wta.hip and wta_hv.hip.
 //
 // Lane k holds S(d) for d in [k*DPL, k*DPL + DPL) as DPL/2 packed u16 pairs
 // (lo half = even d).  The first minimum is a u32 min over keys (S << 16 | d):

@@ -42,7 +42,7 @@ def test_defaults_and_strings(sva):
     p = sva.default_params()
     assert (p.D, p.dmin, p.dir, p.dir_y, p.P1, p.P2, p.subpixel, p.lr_check, p.invalid) == \
         (128, 0, -1, 0, 10, 120, 0, 0, 0xFFFF)
-    assert sva.lib.sva_abi_version() == 4
+    assert sva.lib.sva_abi_version() == 5 == sva.ABI_VERSION
     assert sva.lib.sva_status_string(sva.SVA_ERR_NO_DEVICE) == b"no usable HIP device"
 
 
@@ -57,3 +57,30 @@ def test_no_cpu_fallback_without_device(sva):
 def test_null_context_is_rejected(sva):
     assert sva.lib.sva_synchronize(None) == sva.SVA_ERR_INVALID_ARG
     assert sva.lib.sva_destroy(None) == sva.SVA_ERR_INVALID_ARG
+
+
+def test_tile_stage_sizes_checked_without_device(sva):
+    """the tile stages take byte sizes; a buffer smaller
+    than its plane is SVA_ERR_INVALID_ARG before any device work.
+    sva_tile_check is the entry points' own size test (sva_api.cpp
+    check_tile_buffers), callable without a device."""
+    W, H, D = 1920, 1080, 128
+    lay = sva.tile_layout(W, H, D)
+    assert (lay.seg, lay.nsx, lay.nsy) == (8, 240, 135)
+    assert lay.cost_bytes == W * H * D and lay.diag_bytes == 4 * W * H * D
+    assert lay.hckpt_bytes == 2 * H * 240 * D and lay.vckpt_bytes == 2 * 135 * W * D
+    full = [lay.cost_bytes, lay.diag_bytes, lay.hckpt_bytes, lay.vckpt_bytes]
+    assert sva.lib.sva_tile_check(W, H, D, *full) == sva.SVA_OK
+    for i in range(4):
+        short = list(full)
+        short[i] -= 1
+        assert sva.lib.sva_tile_check(W, H, D, *short) == sva.SVA_ERR_INVALID_ARG, i
+    # ragged sizes: the planes round the segments up
+    lay2 = sva.tile_layout(17, 9, 256)
+    assert (lay2.seg, lay2.nsx, lay2.nsy) == (8, 3, 2)
+    assert sva.lib.sva_tile_check(17, 9, 256, lay2.cost_bytes, lay2.diag_bytes,
+                                  lay2.hckpt_bytes, lay2.vckpt_bytes) == sva.SVA_OK
+    # non-native D and a null context are argument errors too
+    assert sva.lib.sva_tile_check(W, H, 100, *full) == sva.SVA_ERR_INVALID_ARG
+    assert sva.lib.sva_paths_tile_d(None, None, 0, W, H, None, None, 0, None, 0, None, 0) == \
+        sva.SVA_ERR_INVALID_ARG

@@ -27,13 +27,13 @@ def main():
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--dir", type=int, default=-1)
-    ap.add_argument("--sub", action="store_true", help="wta_h / sgm entries: also write the f32 sub-pixel map")
+    ap.add_argument("--sub", action="store_true", help="wta_hv / sgm entries: also write the f32 sub-pixel map")
     ap.add_argument("--dmin", type=int, default=0)
     ap.add_argument("--kernels", action="store_true",
                     help="also report each variant's per-kernel hipEvent averages (timing mode 1 "
                          "on every handle; the event packets slow every variant alike)")
     ap.add_argument("--entry", default="paths",
-                    choices=["paths", "sgm", "cost", "census", "census_cost", "ckpt", "wta_h"])
+                    choices=["paths", "sgm", "cost", "census", "census_cost", "tile", "wta_hv"])
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -50,14 +50,27 @@ def main():
     subm = torch.zeros((H, W), dtype=torch.float32, device=dev)
     C = torch.zeros((H, W, D), dtype=torch.uint8, device=dev)
     L8 = torch.zeros((8, H, W, D), dtype=torch.uint8, device=dev)
-    # checkpoint planes of the ckpt / wta_h entries, full size: sva_paths_ckpt_d
-    # writes [2][H][ns][D] whatever the caller allocated.  Those stage entries
-    # take the native widths only; other D skip them.
+    # the tile stages' planes (ABI v5: sized buffers); native widths only
     native = D in (64, 128, 192, 256)
-    if a.entry in ("ckpt", "wta_h") and not native:
+    if a.entry in ("tile", "wta_hv") and not native:
         raise SystemExit(f"--entry {a.entry} needs D in 64/128/192/256")
-    ns = sva.ckpt_segments(W, D)[0] if native else 0
-    CK = torch.zeros((2, H, ns, D), dtype=torch.uint8, device=dev) if native else None
+    lay = sva.tile_layout(W, H, D) if native else None
+    HCK = torch.zeros(lay.hckpt_bytes, dtype=torch.uint8, device=dev) if native else None
+    VCK = torch.zeros(lay.vckpt_bytes, dtype=torch.uint8, device=dev) if native else None
+    vp = ct.c_void_p
+
+    def tile_call(lib, h):
+        return lib.sva_paths_tile_d(h, vp(C.data_ptr()), ct.c_size_t(C.numel()), W, H,
+                                    ct.byref(p), vp(L8.data_ptr()), ct.c_size_t(L8.numel()),
+                                    vp(HCK.data_ptr()), ct.c_size_t(HCK.numel()),
+                                    vp(VCK.data_ptr()), ct.c_size_t(VCK.numel()))
+
+    def wta_hv_call(lib, h):
+        return lib.sva_wta_hv_d(h, vp(C.data_ptr()), ct.c_size_t(C.numel()), vp(L8.data_ptr()),
+                                ct.c_size_t(L8.numel()), vp(HCK.data_ptr()),
+                                ct.c_size_t(HCK.numel()), vp(VCK.data_ptr()),
+                                ct.c_size_t(VCK.numel()), W, H, ct.byref(p),
+                                vp(disp.data_ptr()), vp(subm.data_ptr()) if a.sub else None)
     p = sva.default_params(D=D, dmin=a.dmin, dir=a.dir, subpixel=1 if a.sub else 0)
     handles = []
     for path in a.libs:
@@ -83,10 +96,9 @@ def main():
                     ct.c_void_p(C_src.data_ptr()))
     torch.cuda.synchronize()
     C_ref = C_src.clone()          # census -> cost bytes, checked against every census_cost variant
-    # checkpoint-mode volumes for the wta_h entry (first library)
+    # tile-stage volumes and checkpoints for the wta_hv entry (first library)
     if native:
-        assert lib0.sva_paths_ckpt_d(h0, ct.c_void_p(C_src.data_ptr()), W, H, ct.byref(p),
-                                     ct.c_void_p(L8.data_ptr()), ct.c_void_p(CK.data_ptr())) == 0
+        assert tile_call(lib0, h0) == 0
     torch.cuda.synchronize()
     times = {n: [] for n, _, _ in handles}
     ref = None
@@ -101,14 +113,10 @@ def main():
             if a.entry == "paths":
                 st = lib.sva_paths_d(h, ct.c_void_p(C.data_ptr()), W, H, ct.byref(p),
                                      ct.c_void_p(L8.data_ptr()))
-            elif a.entry == "ckpt":
-                st = lib.sva_paths_ckpt_d(h, ct.c_void_p(C.data_ptr()), W, H, ct.byref(p),
-                                          ct.c_void_p(L8.data_ptr()), ct.c_void_p(CK.data_ptr()))
-            elif a.entry == "wta_h":
-                st = lib.sva_wta_h_d(h, ct.c_void_p(C.data_ptr()), ct.c_void_p(L8.data_ptr()),
-                                     ct.c_void_p(CK.data_ptr()), W, H, ct.byref(p),
-                                     ct.c_void_p(disp.data_ptr()),
-                                     ct.c_void_p(subm.data_ptr()) if a.sub else None)
+            elif a.entry == "tile":
+                st = tile_call(lib, h)
+            elif a.entry == "wta_hv":
+                st = wta_hv_call(lib, h)
             elif a.entry == "census":
                 st = lib.sva_census_d(h, ct.c_void_p(dL.data_ptr()), W, H, ct.c_size_t(W),
                                       ct.c_void_p(cl.data_ptr()))
@@ -139,22 +147,21 @@ def main():
                 torch.cuda.synchronize()
                 outs.append(torch.sum(C.view(torch.int64)).item())
             assert len(set(outs)) == 1, outs
-        if a.entry in ("ckpt", "wta_h") and it == 0:
+        if a.entry in ("tile", "wta_hv") and it == 0:
             outs = []
             for n, lib, h in handles:
-                if a.entry == "ckpt":
-                    lib.sva_paths_ckpt_d(h, ct.c_void_p(C.data_ptr()), W, H, ct.byref(p),
-                                         ct.c_void_p(L8.data_ptr()), ct.c_void_p(CK.data_ptr()))
+                if a.entry == "tile":
+                    tile_call(lib, h)
                 else:
-                    lib.sva_wta_h_d(h, ct.c_void_p(C.data_ptr()), ct.c_void_p(L8.data_ptr()),
-                                    ct.c_void_p(CK.data_ptr()), W, H, ct.byref(p),
-                                    ct.c_void_p(disp.data_ptr()),
-                                    ct.c_void_p(subm.data_ptr()) if a.sub else None)
+                    wta_hv_call(lib, h)
                 torch.cuda.synchronize()
-                t = L8 if a.entry == "ckpt" else disp
+                t = L8[:4] if a.entry == "tile" else disp
                 outs.append(torch.sum(t.view(torch.int64) if t.dtype == torch.uint8 else
                                       t.to(torch.int64)).item())
-                if a.entry == "wta_h" and a.sub:      # sub-pixel maps bit-identical
+                if a.entry == "tile":
+                    outs[-1] = (outs[-1], torch.sum(HCK.view(torch.int64)).item(),
+                                torch.sum(VCK.view(torch.int64)).item())
+                if a.entry == "wta_hv" and a.sub:      # sub-pixel maps bit-identical
                     outs[-1] = (outs[-1], torch.sum(subm.view(torch.int32).to(torch.int64)).item())
             if not os.environ.get("AB_NOCHECK"):     # ablation builds compute other values
                 assert len(set(outs)) == 1, outs
@@ -185,7 +192,7 @@ def main():
     if a.kernels:
         for n, lib, h in handles:
             ks = {}
-            for k in ("cost", "census", "sgm_paths", "wta_h", "wta_hv"):
+            for k in ("cost", "census", "sgm_paths", "wta_hv"):
                 tot, cnt = ct.c_double(0), ct.c_int64(0)
                 lib.sva_kernel_time(h, k.encode(), ct.byref(tot), ct.byref(cnt))
                 if cnt.value:
