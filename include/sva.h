@@ -143,6 +143,20 @@ int sva_disparity_sgm_d(void* ctx, const uint8_t* left, const uint8_t* right, in
                         int height, size_t pitch, const sva_sgm_params* p, uint16_t* disp,
                         float* subpix);
 
+/* A batch of device-resident frames of one shape on this context's stream:
+ * pair j matches jobs[j].left against jobs[j].right along its own step
+ * (params.dir, params.dir_y), and every frame's cost volume then goes through
+ * ONE sgm_paths and ONE wta_hv launch (up to 8 frames per launch), so small
+ * frames fill the chip (the reference's half-size renders,
+ * CameraStereoVision.cpp:17-18, at the pair loop of :55).  The jobs must share
+ * D, dmin, P1, P2 and subpixel (SVA_ERR_INVALID_ARG otherwise) and may not set
+ * lr_check (SVA_ERR_UNSUPPORTED).  maps: [n][H][W] u16 device; subpix:
+ * [n][H][W] f32 device or NULL.  Results equal sva_disparity_sgm_d per pair.
+ * sva_pair_d is declared with the multi-GPU engine below. */
+struct sva_pair_d;
+int sva_disparity_sgm_batch_d(void* ctx, const struct sva_pair_d* jobs, int n_jobs, int width,
+                              int height, size_t pitch, uint16_t* maps, float* subpix);
+
 /* Stage entry points (device buffers).  Layouts: census W*H u64; C, L
  * [y][x][d] u8; S [y][x][d] u16; L volumes [8][y][x][d] (direction table in
  * DESIGN.md §2.3).  Each buffer must hold exactly its documented shape for

@@ -54,7 +54,7 @@ EXPORTED = [
     "sva_ref_error", "sva_masked_mean_d", "sva_masked_mean", "sva_tile_layout_of",
     "sva_tile_check", "sva_paths_tile_d", "sva_wta_hv_d", "sva_multi_create", "sva_multi_destroy",
     "sva_multi_synchronize", "sva_multi_last_error", "sva_multi_plan", "sva_multi_context",
-    "sva_batch_sgm_d", "sva_array_depth",
+    "sva_batch_sgm_d", "sva_array_depth", "sva_disparity_sgm_batch_d",
 ]
 SVA_MULTI_GATHER_RCCL = 0
 SVA_MULTI_GATHER_PEER = 1
@@ -200,6 +200,7 @@ def _load() -> ct.CDLL:
         "sva_multi_plan": (i32, [i32, i32, i32, P(i32), P(i32), P(i32)]),
         "sva_multi_context": (i32, [vp, i32, i32, P(vp)]),
         "sva_batch_sgm_d": (i32, [vp, P(PairD), i32, i32, i32, sz, vp, vp]),
+        "sva_disparity_sgm_batch_d": (i32, [vp, P(PairD), i32, i32, i32, sz, vp, vp]),
         "sva_array_depth": (i32, [vp, P(vp), i32, i32, i32, sz, P(ArrayPair), i32, P(i32), i32,
                                   dbl, dbl, vp, vp, vp]),
         "sva_resize_linear_f64_d": (i32, [vp, vp, i32, i32, vp, i32, i32]),
@@ -351,6 +352,15 @@ class Context:
     def disparity_sgm_d(self, left, right, W, H, pitch, params, disp, sub=None):
         self._chk(lib.sva_disparity_sgm_d(self.h, _ptr(left), _ptr(right), W, H, pitch,
                                           ct.byref(params), _ptr(disp), _ptr(sub)))
+
+    def disparity_sgm_batch_d(self, pairs, W, H, pitch, maps, sub=None):
+        """pairs: list of (left_ptr, right_ptr, SgmParams) on this context's device;
+        maps: [n][H][W] u16 device, sub: [n][H][W] f32 device or None."""
+        jobs = (PairD * len(pairs))()
+        for i, (l, r, p) in enumerate(pairs):
+            jobs[i] = PairD(_ptr(l), _ptr(r), p)
+        self._chk(lib.sva_disparity_sgm_batch_d(self.h, jobs, len(pairs), W, H, pitch,
+                                                _ptr(maps), _ptr(sub)))
 
     def census_d(self, img, W, H, pitch, out):
         self._chk(lib.sva_census_d(self.h, _ptr(img), W, H, pitch, _ptr(out)))

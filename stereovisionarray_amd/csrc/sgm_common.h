@@ -36,6 +36,10 @@ struct PathGeom {
     size_t ckvol; // bytes of one horizontal checkpoint plane (H*ns*D)
     int nsy;      // vertical checkpoint segments per column, ceil(H / seg)
     size_t ckvvol; // bytes of one vertical checkpoint plane (nsy*W*D)
+    // batched launch: npair frames of the same shape, frame
+    // f's buffers at C + f*cstr, L8 + f*lstr, CK + f*ckstr, CKV + f*ckvstr
+    int npair;
+    size_t cstr, lstr, ckstr, ckvstr;
 };
 
 // Tile-pipeline checkpoints.  With g.ckpt set, the

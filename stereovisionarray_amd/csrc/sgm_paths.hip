@@ -53,9 +53,12 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
                                                                uint8_t* __restrict__ CKV,
                                                                PathGeom g) {
     // Horizontal directions (W steps per line, the longest) get the lowest
-    // block ids and issue priority so they are never the tail.
-    int b = blockIdx.x, r, lb;
-    if (b < 2 * g.blk_h) {
+    // block ids -- every frame's of a batch before any vertical / diagonal
+    // block -- and issue priority so they are never the tail.
+    int b = blockIdx.x, r, lb, f;
+    if (b < 2 * g.blk_h * g.npair) {
+        f = b / (2 * g.blk_h);
+        b -= f * 2 * g.blk_h;
         r = b / g.blk_h;
         lb = b - r * g.blk_h;
         __builtin_amdgcn_s_setprio(1);
@@ -68,9 +71,18 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
         // D=128 (profiles/r03_v3): kernel 0.616-0.622 -> 0.594-0.599 ms, frame
         // 261-263K -> 266-267K Mdisp/s; direction-major had the first-dispatched
         // direction hundreds of steps ahead.
-        b -= 2 * g.blk_h;
+        // (a batch's frames follow one another, each band-major)
+        b -= 2 * g.blk_h * g.npair;
+        f = b / (6 * g.blk_w);
+        b -= f * 6 * g.blk_w;
         r = 2 + b % 6;
         lb = b / 6;
+    }
+    C += (size_t)f * g.cstr;
+    L8 += (size_t)f * g.lstr;
+    if (g.ckpt) {
+        CK += (size_t)f * g.ckstr;
+        CKV += (size_t)f * g.ckvstr;
     }
     const int line = lb * LINES_PER_BLOCK + (threadIdx.x >> 4);
     const int k = threadIdx.x & 15;
@@ -117,7 +129,7 @@ TileGeom tile_geom(int W, int H, int D) {
 }
 
 hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
-                        uint8_t* L8, uint8_t* CK, uint8_t* CKV) {
+                        uint8_t* L8, uint8_t* CK, uint8_t* CKV, int npair) {
     DispatchTimer t(c, "sgm_paths");
     PathGeom g;
     g.W = W; g.H = H; g.D = D; g.P1 = P1; g.P2 = P2;
@@ -132,7 +144,14 @@ hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, i
     g.ns = tg.nsx;
     g.ckvol = tg.hck_bytes / 2;
     if (g.vol >= (size_t)1 << 32) return hipErrorInvalidValue;  // 32-bit buffer offsets
-    dim3 grid(2 * g.blk_h + 6 * g.blk_w);
+    // a batch: npair frames, each with its buffers packed one after another
+    if (npair < 1 || (npair > 1 && !CK)) return hipErrorInvalidValue;
+    g.npair = npair;
+    g.cstr = g.vol;
+    g.lstr = 4 * g.vol;
+    g.ckstr = tg.hck_bytes;
+    g.ckvstr = tg.vck_bytes;
+    dim3 grid((unsigned)((2 * g.blk_h + 6 * g.blk_w) * npair));
 #define SVA_PATHS_LAUNCH(DPL_)                                                               \
     hipExtLaunchKernelGGL(sgm_paths_kernel<DPL_>, grid, dim3(PATH_BLOCK), 0, c.stream, t.start, \
                           t.stop, 0, C, L8, CK, CKV, g);                                    \

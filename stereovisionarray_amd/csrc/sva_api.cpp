@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "sva_internal.h"
+#include "sva_tuning.h"
 
 using namespace sva;
 
@@ -276,6 +277,51 @@ int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int
     return SVA_OK;
 }
 
+// A batch of frames of one shape through one launch of each aggregation
+// kernel: the cost volume of every frame (census + cost per
+// frame, each along its own step), then sgm_paths and wta_hv once over all of
+// them.  jobs[0..n) share D, dmin, P1, P2 and subpixel (checked by the entry
+// point); maps / sub hold n planes of W*H.
+int run_sgm_batch(Ctx* c, const sva_pair_d* jobs, int n, int W, int H, size_t pitch,
+                  uint16_t* maps, float* sub) {
+    const sva_sgm_params* p = &jobs[0].params;
+    const int Dp = padded_D(p->D);
+    const size_t np = (size_t)W * H, nv = np * (size_t)Dp;
+    const TileGeom tg = tile_geom(W, H, Dp);
+    const size_t ckb = tg.hck_bytes + tg.vck_bytes;
+    SVA_HIP(c, c->cost.ensure(nv * n), "cost workspace");
+    SVA_HIP(c, c->paths.ensure(nv * 4 * n), "path workspace");
+    SVA_HIP(c, c->ckpt.ensure(ckb * n), "checkpoint workspace");
+    uint8_t* C = (uint8_t*)c->cost.ptr;
+    for (int i = 0; i < n; i++) {
+        const sva_sgm_params* q = &jobs[i].params;
+        uint8_t* Ci = C + (size_t)i * nv;
+        if (q->dir_y == 0 && Dp >= 128 && census_cost_supported(Dp)) {
+            SVA_HIP(c, launch_census_cost(*c, jobs[i].left, jobs[i].right, W, H, pitch, Dp, q->dmin,
+                                          q->dir, Ci, q->D),
+                    "cost launch");
+        } else {
+            SVA_HIP(c, c->census_l.ensure(np * 8), "census workspace");
+            SVA_HIP(c, c->census_r.ensure(np * 8), "census workspace");
+            uint64_t* cl = (uint64_t*)c->census_l.ptr;
+            uint64_t* cr = (uint64_t*)c->census_r.ptr;
+            SVA_HIP(c, launch_census_pair(*c, jobs[i].left, jobs[i].right, W, H, pitch, cl, cr),
+                    "census launch");
+            SVA_HIP(c, launch_cost2(*c, cl, cr, W, H, Dp, q->dmin, q->dir, q->dir_y, Ci, q->D),
+                    "cost launch");
+        }
+    }
+    uint8_t* L4 = (uint8_t*)c->paths.ptr;
+    uint8_t* CK = (uint8_t*)c->ckpt.ptr;
+    // horizontal planes of all frames, then vertical planes of all frames
+    uint8_t* CKV = CK + tg.hck_bytes * n;
+    SVA_HIP(c, launch_paths(*c, C, W, H, Dp, p->P1, p->P2, L4, CK, CKV, n), "paths launch");
+    SVA_HIP(c, launch_wta_hv(*c, C, L4, CK, CKV, W, H, Dp, p->P1, p->P2, p->dmin, maps,
+                             p->subpixel ? sub : nullptr, p->D, n),
+            "wta launch");
+    return SVA_OK;
+}
+
 int check_camera(Ctx* c, const sva_camera* cam) {
     if (!cam) return fail(c, SVA_ERR_INVALID_ARG, "null camera");
     return SVA_OK;
@@ -523,6 +569,43 @@ int sva_disparity_sgm_d(void* ctx, const uint8_t* left, const uint8_t* right, in
         return s;
     if (!disp) return fail(c, SVA_ERR_INVALID_ARG, "null disparity output");
     return run_sgm_device(c, left, right, W, H, pitch, p, disp, p->subpixel ? sub : nullptr);
+}
+
+int sva_disparity_sgm_batch_d(void* ctx, const sva_pair_d* jobs, int n, int W, int H,
+                              size_t pitch, uint16_t* maps, float* sub) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    if (!jobs || n <= 0 || !maps) return fail(c, SVA_ERR_INVALID_ARG, "bad batch argument");
+    int s;
+    const sva_sgm_params* p0 = &jobs[0].params;
+    for (int i = 0; i < n; i++) {
+        const sva_sgm_params* q = &jobs[i].params;
+        if ((s = check_image(c, jobs[i].left, W, H, pitch)) ||
+            (s = check_image(c, jobs[i].right, W, H, pitch)) || (s = check_sgm(c, q, W, H)))
+            return s;
+        if (q->D != p0->D || q->dmin != p0->dmin || q->P1 != p0->P1 || q->P2 != p0->P2 ||
+            q->subpixel != p0->subpixel)
+            return fail(c, SVA_ERR_INVALID_ARG,
+                        "a batch's pairs must share D, dmin, P1, P2 and subpixel");
+        if (q->lr_check) return fail(c, SVA_ERR_UNSUPPORTED, "the batch route has no L/R check");
+    }
+    if (!wta_hv_supported(padded_D(p0->D)))
+        return fail(c, SVA_ERR_UNSUPPORTED, "no tile pipeline for this D");
+    // chunks of at most tune::kBatchMaxPairs frames, whose workspaces stay
+    // under tune::kBatchMaxBytes
+    const int Dp = padded_D(p0->D);
+    const TileGeom tg = tile_geom(W, H, Dp);
+    const size_t per = (size_t)W * H * (size_t)Dp * 5 + tg.hck_bytes + tg.vck_bytes;
+    int chunk = tune::kBatchMaxPairs;
+    while (chunk > 1 && per * (size_t)chunk > tune::kBatchMaxBytes) chunk--;
+    const size_t np = (size_t)W * H;
+    for (int i0 = 0; i0 < n; i0 += chunk) {
+        const int m = std::min(chunk, n - i0);
+        if ((s = run_sgm_batch(c, jobs + i0, m, W, H, pitch, maps + (size_t)i0 * np,
+                               sub ? sub + (size_t)i0 * np : nullptr)))
+            return s;
+    }
+    return SVA_OK;
 }
 
 int sva_disparity_sgm(void* ctx, const uint8_t* left, const uint8_t* right, int W, int H,

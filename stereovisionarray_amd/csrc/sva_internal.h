@@ -139,9 +139,12 @@ hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, in
 // sgm_paths.hip -- all 8 directions in one launch.  CK == CKV == nullptr:
 // L8 = [8][H][W][D] u8.  CK and CKV set (the tile pipeline):
 // L8 = [4][H][W][D] (directions 4..7), CK = [2][H][nsx][D] and CKV =
-// [2][nsy][W][D] (tile_geom below).
+// [2][nsy][W][D] (tile_geom below).  npair > 1 (tile pipeline only): a batch
+// of frames in one launch, each buffer holding npair such planes back to back
+// (DESIGN.md §4.10).
 hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
-                        uint8_t* L8, uint8_t* CK = nullptr, uint8_t* CKV = nullptr);
+                        uint8_t* L8, uint8_t* CK = nullptr, uint8_t* CKV = nullptr,
+                        int npair = 1);
 // Tile pipeline geometry: tiles of 16 columns x seg rows (seg = 2^seg_log2),
 // checkpoints every seg columns (horizontal lines) and every seg rows
 // (vertical lines).
@@ -166,7 +169,7 @@ inline int padded_D(int D) {
 bool wta_hv_supported(int D);
 hipError_t launch_wta_hv(Ctx& c, const uint8_t* C, const uint8_t* L4, const uint8_t* CK,
                          const uint8_t* CKV, int W, int H, int D, int P1, int P2, int dmin,
-                         uint16_t* disp, float* sub, int dreal = 0);
+                         uint16_t* disp, float* sub, int dreal = 0, int npair = 1);
 // wta.hip
 hipError_t launch_sum(Ctx& c, const uint8_t* L8, int W, int H, int D, uint16_t* S);
 hipError_t launch_wta_from_sum(Ctx& c, const uint16_t* S, int W, int H, int D, int dmin,

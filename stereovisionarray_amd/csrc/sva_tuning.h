@@ -7,6 +7,8 @@
 // A/B library never shares a translation unit with the product.
 #pragma once
 
+#include <cstddef>
+
 namespace sva {
 namespace tune {
 
@@ -94,6 +96,12 @@ constexpr int kWtahvPinWta = 1;
 // -> 0.2495 / 0.2450 ms, D=64 0.150 -> 0.144, D=192 0.393 -> 0.380, D=256
 // 0.556 -> 0.538, 4K D=256 2.215 -> 2.158.
 constexpr int kWtahvSubLds = 1;
+
+// ---- batched frames (sva_disparity_sgm_batch_d) ----------
+// Frames per sgm_paths / wta_hv launch, and the workspace those frames may
+// hold (cost + 4 diagonal volumes + checkpoints per frame).
+constexpr int kBatchMaxPairs = 8;
+constexpr size_t kBatchMaxBytes = (size_t)24 << 30;
 
 // ---- census.hip / census_cost.hip / cost.hip ------------
 // Rows per workgroup of the multi-row census kernel.

@@ -43,6 +43,7 @@ struct WtaHvGeom {
     unsigned vol;     // bytes of one [H][W][D] volume (< 2^32)
     unsigned hck;     // bytes of one horizontal checkpoint plane [H][nsx][D]
     unsigned vck;     // bytes of one vertical checkpoint plane [nty][W][D]
+    int tiles;        // tiles per frame, ntx * nty (a batch: frame = block / tiles)
 };
 
 // Prefetch depth (pixels) of the diagonal volumes in the last pass.
@@ -67,8 +68,17 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
 
     constexpr int SPR = TW / TY;        // phase H: row segments per tile row
     static_assert(TY <= TW && TW % TY == 0, "tile rows must divide 16");
-    const int tx = (int)(blockIdx.x % (unsigned)g.ntx);
-    const int ty = (int)(blockIdx.x / (unsigned)g.ntx);
+    // a batch of frames: frame f's planes follow frame f-1's
+    const unsigned f = blockIdx.x / (unsigned)g.tiles;
+    const unsigned tb = blockIdx.x - f * (unsigned)g.tiles;
+    const int tx = (int)(tb % (unsigned)g.ntx);
+    const int ty = (int)(tb / (unsigned)g.ntx);
+    C += (size_t)f * g.vol;
+    L4 += (size_t)f * 4 * g.vol;
+    CK += (size_t)f * 2 * g.hck;
+    CKV += (size_t)f * 2 * g.vck;
+    disp += (size_t)f * (size_t)g.W * (size_t)g.H;
+    if (sub) sub += (size_t)f * (size_t)g.W * (size_t)g.H;
     const int slot = (int)(threadIdx.x >> 4);
     const int k = (int)(threadIdx.x & 15);
     const int W = g.W, H = g.H;
@@ -322,7 +332,7 @@ bool wta_hv_supported(int D) { return D == 64 || D == 128 || D == 192 || D == 25
 
 hipError_t launch_wta_hv(Ctx& c, const uint8_t* C, const uint8_t* L4, const uint8_t* CK,
                          const uint8_t* CKV, int W, int H, int D, int P1, int P2, int dmin,
-                         uint16_t* disp, float* sub, int dreal) {
+                         uint16_t* disp, float* sub, int dreal, int npair) {
     DispatchTimer t(c, "wta_hv");
     if (!wta_hv_supported(D)) return hipErrorInvalidValue;
     const TileGeom tg = tile_geom(W, H, D);
@@ -338,7 +348,9 @@ hipError_t launch_wta_hv(Ctx& c, const uint8_t* C, const uint8_t* L4, const uint
     g.hck = (unsigned)(tg.hck_bytes / 2);
     g.vck = (unsigned)(tg.vck_bytes / 2);
     const bool pad = g.dreal < D;
-    const dim3 grid((unsigned)(g.ntx * g.nty));
+    if (npair < 1) return hipErrorInvalidValue;
+    g.tiles = g.ntx * g.nty;
+    const dim3 grid((unsigned)(g.tiles * npair));
 #define SVA_WTAHV(DPL_, TYL_)                                                                 \
     if (pad)                                                                                  \
         hipExtLaunchKernelGGL((wta_hv_kernel<DPL_, TYL_, true>), grid, dim3(TB), 0, c.stream, \

@@ -1,0 +1,109 @@
+"""The batched frame route (sva_disparity_sgm_batch_d): n
+frames of one shape through one sgm_paths and one wta_hv launch.  Every
+frame's map and sub-pixel map must equal the single-frame route's
+(sva_disparity_sgm_d) bit for bit, which the rest of the suite pins to the
+oracle; a few frames are checked against the oracle directly.  Frames differ
+in their step (1-D and 2-D, both signs), batches run past the 8-frame chunk,
+and mismatched parameters are refused."""
+import numpy as np
+import pytest
+import torch
+
+from stereovisionarray_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+STEPS = [(-1, 0), (1, 0), (0, -1), (0, 1), (-1, -1), (1, 1), (-2, -1), (1, -1), (-1, 1)]
+
+
+def frames(H, W, D, n, seed):
+    out = []
+    for i in range(n):
+        sx, sy = STEPS[i % len(STEPS)]
+        if sy == 0:
+            L, R, _ = synth.stereo_pair(H, W, D, 0, sx, seed=seed + i, stripes=4, step=5)
+        else:
+            L, R, _ = synth.stereo_pair2(H, W, D, 0, sx, sy, seed=seed + i, stripes=4, step=5)
+        out.append((L, R, sx, sy))
+    return out
+
+
+def run_batch(ctx, sva, torch_dev, fr, D, subpixel=1, dmin=0):
+    H, W = fr[0][0].shape
+    dl = [torch.from_numpy(L).to(torch_dev) for L, _, _, _ in fr]
+    dr = [torch.from_numpy(R).to(torch_dev) for _, R, _, _ in fr]
+    n = len(fr)
+    pairs = [(dl[i].data_ptr(), dr[i].data_ptr(),
+              sva.default_params(D=D, dmin=dmin, dir=fr[i][2], dir_y=fr[i][3], subpixel=subpixel))
+             for i in range(n)]
+    maps = torch.full((n, H, W), 0x5A5A, dtype=torch.int16, device=torch_dev)
+    sub = torch.zeros((n, H, W), dtype=torch.float32, device=torch_dev)
+    ctx.disparity_sgm_batch_d(pairs, W, H, W, maps.data_ptr(), sub.data_ptr())
+    one = torch.zeros((H, W), dtype=torch.int16, device=torch_dev)
+    one_sub = torch.zeros((H, W), dtype=torch.float32, device=torch_dev)
+    ref_m, ref_s = [], []
+    for i in range(n):
+        ctx.disparity_sgm_d(dl[i].data_ptr(), dr[i].data_ptr(), W, H, W, pairs[i][2],
+                            one.data_ptr(), one_sub.data_ptr())
+        ctx.synchronize()
+        ref_m.append(one.cpu().numpy().copy())
+        ref_s.append(one_sub.cpu().numpy().copy())
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    return maps.cpu().numpy(), sub.cpu().numpy(), ref_m, ref_s
+
+
+@pytest.mark.parametrize("D", [64, 128, 192, 256])
+@pytest.mark.parametrize("H,W", [(40, 77), (17, 130), (64, 64)])
+def test_batch_equals_single_frames(ctx, sva, torch_dev, D, H, W):
+    fr = frames(H, W, D, 5, seed=H * W + D)
+    maps, sub, ref_m, ref_s = run_batch(ctx, sva, torch_dev, fr, D)
+    for i in range(len(fr)):
+        assert np.array_equal(maps[i], ref_m[i]), f"frame {i} step {fr[i][2:]}"
+        assert np.array_equal(sub[i].view(np.uint32), ref_s[i].view(np.uint32)), f"sub {i}"
+
+
+def test_batch_past_one_chunk_and_padded_D(ctx, sva, torch_dev):
+    """11 frames (two launches of 8 + 3), D = 100 (run at 128, padded)."""
+    fr = frames(33, 90, 100, 11, seed=5)
+    maps, sub, ref_m, ref_s = run_batch(ctx, sva, torch_dev, fr, 100)
+    for i in range(len(fr)):
+        assert np.array_equal(maps[i], ref_m[i]), i
+        assert np.array_equal(sub[i].view(np.uint32), ref_s[i].view(np.uint32)), i
+
+
+def test_batch_against_oracle(ctx, sva, oracle, torch_dev):
+    D, H, W = 64, 30, 110
+    fr = frames(H, W, D, 4, seed=9)
+    maps, sub, _, _ = run_batch(ctx, sva, torch_dev, fr, D, dmin=2)
+    for i, (L, R, sx, sy) in enumerate(fr):
+        od, osub = oracle.sgm2(L, R, D, 2, sx, sy, subpixel=True)
+        assert np.array_equal(maps[i].view(np.uint16), od), i
+        assert np.max(np.abs(sub[i] - osub)) <= 1e-5, i
+
+
+def test_batch_without_subpixel(ctx, sva, torch_dev):
+    fr = frames(20, 50, 64, 3, seed=2)
+    maps, sub, ref_m, _ = run_batch(ctx, sva, torch_dev, fr, 64, subpixel=0)
+    for i in range(3):
+        assert np.array_equal(maps[i], ref_m[i])
+    assert (sub == 0).all()
+
+
+def test_batch_refuses_mixed_params(ctx, sva, torch_dev):
+    H, W = 16, 40
+    a = torch.zeros((H, W), dtype=torch.uint8, device=torch_dev)
+    maps = torch.zeros((2, H, W), dtype=torch.int16, device=torch_dev)
+    p0 = sva.default_params(D=64)
+    for bad, status in ((sva.default_params(D=128), sva.SVA_ERR_INVALID_ARG),
+                        (sva.default_params(D=64, dmin=3), sva.SVA_ERR_INVALID_ARG),
+                        (sva.default_params(D=64, P2=100), sva.SVA_ERR_INVALID_ARG),
+                        (sva.default_params(D=64, lr_check=1), sva.SVA_ERR_UNSUPPORTED)):
+        with pytest.raises(sva.SvaError) as e:
+            ctx.disparity_sgm_batch_d([(a.data_ptr(), a.data_ptr(), p0),
+                                       (a.data_ptr(), a.data_ptr(), bad)], W, H, W,
+                                      maps.data_ptr())
+        assert e.value.status == status
+    with pytest.raises(sva.SvaError) as e:
+        ctx.disparity_sgm_batch_d([], W, H, W, maps.data_ptr())
+    assert e.value.status == sva.SVA_ERR_INVALID_ARG
