@@ -83,6 +83,10 @@ def parse():
                     help="pairs of a step go round-robin to this many contexts, each with its "
                          "own HIP stream and workspaces, so pairs overlap (0 = auto: 2 when a "
                          "rank has several pairs per step and D != 192, else 1)")
+    ap.add_argument("--batch", action="store_true",
+                    help="a rank's pairs of a step go through sva_disparity_sgm_batch_d on one "
+                         "context: one sgm_paths and one wta_hv launch per 8 frames "
+                         "(DESIGN.md §4.10) instead of one launch each on --streams contexts")
     ap.add_argument("--no-overlap", action="store_true",
                     help="gather each step's maps synchronously on the compute stream")
     ap.add_argument("--rehearse-overlap", action="store_true",
@@ -478,13 +482,13 @@ def kernel_table(ctx, names=("census", "cost", "sgm_paths", "wta_hv", "fuse_dept
 # Algorithmic bytes per launch of the path-aggregation kernel:
 # SURVEY.md §8(d)'s aggregation model, 10 B/disp (8 u8 C reads + one u16 S
 # write), whatever the kernel spills.
-def roofline_of(kernels, W, H, D, workload, overlapped=False):
+def roofline_of(kernels, W, H, D, workload, overlapped=False, frames_per_launch=1):
     name = "sgm_paths"
     agg = kernels.get(name)
     if not agg:
         return None
     model = "SURVEY §8d aggregation: 10 B/disp"
-    alg_bytes = AGG_BYTES_PER_DISP * W * H * D
+    alg_bytes = AGG_BYTES_PER_DISP * W * H * D * frames_per_launch
     achieved = alg_bytes / (agg["avg_ms"] * 1e-3) / 1e9
     out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -495,6 +499,8 @@ def roofline_of(kernels, W, H, D, workload, overlapped=False):
         # pairs overlap on several streams: a launch's event span includes the
         # other stream's kernels, so this fraction is not the single-stream one
         out["overlapped"] = True
+    if frames_per_launch != 1:
+        out["frames_per_launch"] = frames_per_launch
     return out
 
 
@@ -505,13 +511,15 @@ def roofline_of(kernels, W, H, D, workload, overlapped=False):
 # timed-region hipEvent averages, so moving work between the two kernels
 # cannot move the grade.
 AGG_KERNELS = ("sgm_paths", "wta_hv")
+BATCH_MAX_PAIRS = 8    # frames per launch of sva_disparity_sgm_batch_d (sva_tuning.h)
 
 
-def aggregation_roofline_of(kernels, W, H, D, traffic_per_kernel=None, overlapped=False):
+def aggregation_roofline_of(kernels, W, H, D, traffic_per_kernel=None, overlapped=False,
+                            frames_per_launch=1):
     if not all(k in kernels for k in AGG_KERNELS):
         return None
     ms = sum(kernels[k]["avg_ms"] for k in AGG_KERNELS)
-    alg = (AGG_BYTES_PER_DISP + 2.0) * W * H * D + 2.0 * W * H
+    alg = ((AGG_BYTES_PER_DISP + 2.0) * W * H * D + 2.0 * W * H) * frames_per_launch
     ach = alg / (ms * 1e-3) / 1e9
     out = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
@@ -525,6 +533,8 @@ def aggregation_roofline_of(kernels, W, H, D, traffic_per_kernel=None, overlappe
         out["traffic_over_alg"] = round(out["traffic"] / alg, 3)
     if overlapped:
         out["overlapped"] = True
+    if frames_per_launch != 1:
+        out["frames_per_launch"] = frames_per_launch
     return out
 
 
@@ -606,6 +616,8 @@ def run_array(a, wl, world, rank, local, dev):
     # 311.2-315.0K (2) -> 319.7-321.0K (3) -> 309.3K (4) Mdisp/s; grid8_all
     # 316.2-316.9K (2) -> 316.4-318.1K (3) -> 305.2-308.1K (4).
     n_streams = a.streams if a.streams > 0 else (min(3, len(jobs)) if len(jobs) > 1 else 1)
+    if a.batch:
+        n_streams = 1                    # the batch runs on one context
     ctxs, cstreams = [ctx], [stream]
     for _ in range(1, n_streams):
         s_ = torch.cuda.Stream(dev)
@@ -651,9 +663,13 @@ def run_array(a, wl, world, rank, local, dev):
             go.record(stream)
             for s_ in cstreams[1:]:
                 s_.wait_event(go)
-        for jb, (L, R, p) in enumerate(jobs):
-            ctxs[jb % len(ctxs)].disparity_sgm_d(L.data_ptr(), R.data_ptr(), W, H, W, p,
-                                                 dsp[jb].data_ptr())
+        if a.batch:
+            ctx.disparity_sgm_batch_d([(L.data_ptr(), R.data_ptr(), p) for (L, R, p) in jobs],
+                                      W, H, W, dsp.data_ptr())
+        else:
+            for jb, (L, R, p) in enumerate(jobs):
+                ctxs[jb % len(ctxs)].disparity_sgm_d(L.data_ptr(), R.data_ptr(), W, H, W, p,
+                                                     dsp[jb].data_ptr())
         for s_ in cstreams[1:]:
             done_ = torch.cuda.Event()
             done_.record(s_)
@@ -689,6 +705,11 @@ def run_array(a, wl, world, rank, local, dev):
     value = n_units * W * H * D * a.steps / elapsed / 1e6
     # committed PMC bytes per pair: the 1080p D=128 frame's for the 1080p rigs
     traffic_wl = "1080p_d128" if (W, H, D) == (1920, 1080, 128) else a.workload
+    if a.batch:   # frames per aggregation launch: the mean over this rank's launches
+        n_launch = -(-len(jobs) // BATCH_MAX_PAIRS)
+        fpl = len(jobs) / n_launch
+    else:
+        fpl = 1
     exchange = None
     if multi:
         def recompute(u):
@@ -739,14 +760,16 @@ def run_array(a, wl, world, rank, local, dev):
                        "W": W, "H": H, "D": D, "P1": 10, "P2": 120, "pairs": n_units,
                        "parallelism": f"pairs sharded over {world} rank(s), gather to rank 0"
                                       + (" overlapped with the next step" if overlap else ""),
-                       "streams_per_rank": len(ctxs)},
+                       "streams_per_rank": len(ctxs), "batched": bool(a.batch)},
             "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
             "fused_maps_per_s": round(len(groups) * a.steps / elapsed, 2),
             "ref_interior_depth_exact_frac": round(exact, 4),
-            "roofline": roofline_of(kernels, W, H, D, traffic_wl, overlapped=len(ctxs) > 1),
+            "roofline": roofline_of(kernels, W, H, D, traffic_wl, overlapped=len(ctxs) > 1,
+                                    frames_per_launch=fpl),
             "aggregation_roofline": aggregation_roofline_of(kernels, W, H, D,
                                                             committed_traffic(traffic_wl),
-                                                            overlapped=len(ctxs) > 1),
+                                                            overlapped=len(ctxs) > 1,
+                                                            frames_per_launch=fpl),
             "cpu_baseline": None,
         }
         if exchange is not None:
@@ -1031,6 +1054,8 @@ def main():
     # two streams win there too: 304.9-307.7K -> 317.9K Mdisp/s
     # (profiles/r03_v8/streams_batch256.log.txt).
     n_streams = a.streams if a.streams > 0 else (1 if P == 1 else 2)
+    if a.batch:
+        n_streams = 1                    # the batch runs on one context
     ctx = sva.Context(local)
     stream = torch.cuda.Stream(dev)     # non-default stream shared by kernels, copies, RCCL
     torch.cuda.set_stream(stream)
@@ -1054,6 +1079,7 @@ def main():
         L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=seed0 + u)
         lefts.append(torch.from_numpy(L).to(dev))
         rights.append(torch.from_numpy(R).to(dev))
+    batch_jobs = [(lefts[j].data_ptr(), rights[j].data_ptr(), params) for j in range(P)]
     # Two map buffers: step i computes into buffer i%2 on the compute stream
     # while the gather of step i-1 (buffer (i-1)%2) runs on a comm stream.
     overlap = (world > 1 and a.dist_backend == "nccl" and not a.no_overlap) or \
@@ -1086,9 +1112,13 @@ def main():
             go.record(stream)
             for s_ in cstreams[1:]:
                 s_.wait_event(go)
-        for j in range(P):
-            ctxs[j % len(ctxs)].disparity_sgm_d(lefts[j].data_ptr(), rights[j].data_ptr(), W, H,
-                                                W, params, disp[j].data_ptr(), sub[j].data_ptr())
+        if a.batch:
+            ctx.disparity_sgm_batch_d(batch_jobs, W, H, W, disp.data_ptr(), sub.data_ptr())
+        else:
+            for j in range(P):
+                ctxs[j % len(ctxs)].disparity_sgm_d(lefts[j].data_ptr(), rights[j].data_ptr(), W,
+                                                    H, W, params, disp[j].data_ptr(),
+                                                    sub[j].data_ptr())
         for s_ in cstreams[1:]:
             done_ = torch.cuda.Event()
             done_.record(s_)
@@ -1132,7 +1162,9 @@ def main():
     disparities = units * W * H * D
     value = disparities / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1e3
-    roofline = roofline_of(kernels, W, H, D, a.workload, overlapped=len(ctxs) > 1)
+    fpl = P / -(-P // BATCH_MAX_PAIRS) if a.batch else 1
+    roofline = roofline_of(kernels, W, H, D, a.workload, overlapped=len(ctxs) > 1,
+                           frames_per_launch=fpl)
     out = {
         "metric": "Mdisparities/sec (W·H·D/s) at 1080p D=128" if a.workload == "1080p_d128"
                   else f"Mdisparities/sec (W·H·D/s) {a.workload}",
@@ -1152,11 +1184,12 @@ def main():
                    "W": W, "H": H, "D": D, "P1": 10, "P2": 120,
                    "parallelism": f"pairs sharded over {world} rank(s), RCCL gather to rank 0"
                                   + (" overlapped with the next step" if nbuf == 2 else ""),
-                   "streams_per_rank": len(ctxs)},
+                   "streams_per_rank": len(ctxs), "batched": bool(a.batch)},
         "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
         "roofline": roofline,
         "aggregation_roofline": aggregation_roofline_of(kernels, W, H, D, committed_traffic(a.workload),
-                                                        overlapped=len(ctxs) > 1),
+                                                        overlapped=len(ctxs) > 1,
+                                                        frames_per_launch=fpl),
         "cpu_baseline": None,
     }
     if len(ctxs) == 1:

@@ -102,7 +102,7 @@ int main(int argc, char** argv) {
     std::printf("TO_CENTER_SMALL: 8 pairs + fusion in %.2f ms; fused depth at the centre %.4f m "
                 "from %d maps\n", ms(t0), fused[pc], nv[pc]);
 
-    // Refinement (functions.cpp:11-48) of the Mode R map with the CROSS pairs
+    // Refinement (functions.cpp:11-52) of the Mode R map with the CROSS pairs
     std::vector<std::array<Camera, 2>> camPairs;
     std::vector<ImageView> pairImages;
     for (auto& pr : getCameraPairs(cameras, CROSS)) {

@@ -237,7 +237,7 @@ int sva_ref_endpoints_d(void* ctx, int width, int height, const sva_camera* ref_
  * routine does not write keep the caller's buffer contents (the reference
  * leaves them uninitialised). */
 
-/* shiftPerspectiveWithDisparity (functions.cpp:50-72): shifted(x, y) =
+/* shiftPerspectiveWithDisparity (functions.cpp:55-77): shifted(x, y) =
  * image((int)(d*preX + x), (int)(d*preY + y)) for d = disparity(x, y) != 0,
  * pre = (in.pos - out.pos) / |in.pos - out.pos|. */
 int sva_shift_perspective_d(void* ctx, const sva_camera* in_cam, const sva_camera* out_cam,
@@ -247,7 +247,7 @@ int sva_shift_perspective(void* ctx, const sva_camera* in_cam, const sva_camera*
                           const uint8_t* disparity, const uint8_t* image, int width, int height,
                           size_t pitch, uint8_t* shifted);
 
-/* improveWithDisparity (functions.cpp:11-48): for each pair i (cam_pairs[2i],
+/* improveWithDisparity (functions.cpp:11-52): for each pair i (cam_pairs[2i],
  * cam_pairs[2i+1], paired image images[i]) shift the image by the disparity,
  * then re-search 11 candidates along the 0/1 direction with 2k x 2k SADs,
  * k = (window_size-1)/2 <= 32; the last pair wins.  mask nullable (= the
@@ -264,7 +264,7 @@ int sva_improve_with_disparity(void* ctx, const uint8_t* disparity, const uint8_
                                int n_pairs, int width, int height, size_t pitch,
                                const uint8_t* mask, int window_size, int strict, uint8_t* out);
 
-/* shiftPerspective2 (functions.cpp:74-97): depth >= 0.5 scattered to
+/* shiftPerspective2 (functions.cpp:79-103): depth >= 0.5 scattered to
  * (x + (int)(preX/depth), y + (int)(preY/depth)), pre = (in.pos - out.pos)*f/ps;
  * collisions resolve to the last write of the reference's x-major loop. */
 int sva_shift_perspective2_d(void* ctx, const sva_camera* in_cam, const sva_camera* out_cam,

@@ -503,7 +503,7 @@ inline std::vector<std::vector<double>> computeArrayDepth(
 
 static_assert(sizeof(Point3d) == 3 * sizeof(double), "Point3d must be three packed doubles");
 
-// shiftPerspectiveWithDisparity -- functions.cpp:50-72.
+// shiftPerspectiveWithDisparity -- functions.cpp:55-77.
 inline std::vector<uint8_t> shiftPerspectiveWithDisparity(Engine& eng, const Camera& inputCam,
                                                           const Camera& outputCam,
                                                           const ImageView& disparity,
@@ -519,7 +519,7 @@ inline std::vector<uint8_t> shiftPerspectiveWithDisparity(Engine& eng, const Cam
     return init;
 }
 
-// improveWithDisparity -- functions.cpp:11-48.  `mask` replaces
+// improveWithDisparity -- functions.cpp:11-52.  `mask` replaces
 // getFaceMask(centerImage) (:13; empty view = every pixel).  strict (default,
 // as the reference): a masked pixel whose window leaves the image throws
 // sva::Error, the analogue of the reference's cv::Exception on that ROI.
@@ -553,7 +553,7 @@ inline std::vector<uint8_t> improveWithDisparity(Engine& eng, const ImageView& d
     return init;
 }
 
-// shiftPerspective2 -- functions.cpp:74-97 (depth map W*H f64).
+// shiftPerspective2 -- functions.cpp:79-103 (depth map W*H f64).
 inline std::vector<double> shiftPerspective2(Engine& eng, const Camera& inputCam,
                                              const Camera& outputCam,
                                              const std::vector<double>& depthMap, int W, int H,

@@ -34,7 +34,7 @@ static int to_int(double v, long long* out) {
     return 1;
 }
 
-/* shiftPerspectiveWithDisparity (functions.cpp:50-72). */
+/* shiftPerspectiveWithDisparity (functions.cpp:55-77). */
 void svo_shift_perspective(const svo_camera* in, const svo_camera* out, const uint8_t* disp,
                            const uint8_t* img, int W, int H, ptrdiff_t pitch, uint8_t* shifted) {
     double n = norm3(in->pos, out->pos);
@@ -64,7 +64,7 @@ static int64_t sad_win(const uint8_t* a, const uint8_t* b, ptrdiff_t pitch, int 
     return s;
 }
 
-/* improveWithDisparity (functions.cpp:11-48).  cams = [n][2] (cam[0], cam[1]
+/* improveWithDisparity (functions.cpp:11-52).  cams = [n][2] (cam[0], cam[1]
  * of each pair), images[c] = the image paired with the centre view.  strict:
  * return -1 at the first masked pixel whose window leaves the image (the
  * reference's cv::Mat ROI throws there); otherwise such pixels are skipped.
@@ -112,7 +112,7 @@ int svo_improve_with_disparity(const uint8_t* disp, const uint8_t* center,
     return 0;
 }
 
-/* shiftPerspective2 (functions.cpp:74-97): scatter, x-major loop, last write
+/* shiftPerspective2 (functions.cpp:79-103): scatter, x-major loop, last write
  * wins; depth < 0.5 skipped. */
 void svo_shift_perspective2(const svo_camera* in, const svo_camera* out, const double* depth,
                             int W, int H, double* shifted) {

@@ -152,18 +152,18 @@ void svo_fuse_depth(const uint16_t* disps, int n_maps, int W, int H, const doubl
 /* Semantics for the reference's undefined corners: refine_oracle.c header,
  * DESIGN.md §2.7.  Pixels a loop skips keep the caller's buffer contents. */
 
-/* shiftPerspectiveWithDisparity (functions.cpp:50-72): gather. */
+/* shiftPerspectiveWithDisparity (functions.cpp:55-77): gather. */
 void svo_shift_perspective(const svo_camera* in, const svo_camera* out, const uint8_t* disp,
                            const uint8_t* img, int W, int H, ptrdiff_t pitch, uint8_t* shifted);
 
-/* improveWithDisparity (functions.cpp:11-48); cams = [n][2]; returns 0, or -1
+/* improveWithDisparity (functions.cpp:11-52); cams = [n][2]; returns 0, or -1
  * when strict and a masked pixel's window leaves the image (reference throws). */
 int svo_improve_with_disparity(const uint8_t* disp, const uint8_t* center,
                                const uint8_t* const* images, const svo_camera* cams, int n,
                                int W, int H, ptrdiff_t pitch, const uint8_t* mask, int window,
                                int strict, uint8_t* out);
 
-/* shiftPerspective2 (functions.cpp:74-97): scatter, last write in x-major order wins. */
+/* shiftPerspective2 (functions.cpp:79-103): scatter, last write in x-major order wins. */
 void svo_shift_perspective2(const svo_camera* in, const svo_camera* out, const double* depth,
                             int W, int H, double* shifted);
 

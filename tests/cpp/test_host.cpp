@@ -233,7 +233,7 @@ static void gpu_tests() {
         CHECK(fuseDepth(eng, single, W, H, bl, cams[12].f, cams[12].pixel_size) == fused[0]);
     }
 
-    // refinement: img(x) = centre(x - dd - 2) => refined disparity dd + 2 (functions.cpp:11-48)
+    // refinement: img(x) = centre(x - dd - 2) => refined disparity dd + 2 (functions.cpp:11-52)
     const int dd = 6;
     std::vector<uint8_t> other(W * H, 0), dispc(W * H, dd), fmask(W * H, 0);
     for (int y = 0; y < H; y++)

@@ -323,7 +323,7 @@ def _cam(oracle, f, pos, ps):
 
 
 def test_shift_perspective_kat(oracle):
-    """functions.cpp:50-72: pre = (in - out) / |in - out|; gather at
+    """functions.cpp:55-77: pre = (in - out) / |in - out|; gather at
     ((int)(d*preX + x), (int)(d*preY + y)); d == 0 and out-of-range keep init."""
     c12 = _cam(oracle, 0.05, (0, 0, -0.75), 1e-4)
     c11 = _cam(oracle, 0.05, (-0.05, 0, -0.75), 1e-4)
@@ -338,7 +338,7 @@ def test_shift_perspective_kat(oracle):
 
 
 def test_improve_with_disparity_kat(oracle):
-    """functions.cpp:11-48 by construction: with disp = d0 and the paired image
+    """functions.cpp:11-52 by construction: with disp = d0 and the paired image
     img(x) = centre(x - d0 - 2), the shifted image is centre(x - 2), so
     candidate p = 7 matches exactly and the refined disparity is d0 + 2."""
     W, H, d0 = 64, 24, 6
@@ -369,7 +369,7 @@ def test_improve_with_disparity_kat(oracle):
 
 
 def test_shift_perspective2_kat(oracle):
-    """functions.cpp:74-97: preX = 0.05*0.05/1e-3 = 2.5 (to f64 rounding);
+    """functions.cpp:79-103: preX = 0.05*0.05/1e-3 = 2.5 (to f64 rounding);
     depth 1 at x=0 -> +int(2.5) = 2; depth 2 at x=1 -> +int(1.25) = 1: both
     land on x=2, the later x (loop order) wins; depth < 0.5 skipped."""
     cin = _cam(oracle, 0.05, (0.05, 0, 0), 1e-3)

@@ -4,7 +4,8 @@ stereovisionarray_amd/csrc with literal text replacements applied:
 
     tools/build_patch_variant.py NAME FILE 'OLD' 'NEW' [FILE 'OLD' 'NEW' ...]
 
-Each OLD must occur in FILE (all occurrences are replaced).  Output:
+Each OLD must occur in FILE (all occurrences are replaced); OLD = '@' copies
+the file at path NEW over FILE.  Output:
 ab_libs/libsva_NAME.so; the product sources and libsva.so are untouched.
 Ablation builds compute other values on purpose (run tools/ab_paths.py with
 AB_NOCHECK=1)."""
@@ -26,6 +27,9 @@ def main():
     for i in range(0, len(rest), 3):
         f, old, new = rest[i:i + 3]
         p = os.path.join(src, f)
+        if old == "@":                 # replace the whole file by NEW (a path)
+            shutil.copy(new, p)
+            continue
         t = open(p).read()
         if old not in t:
             raise SystemExit(f"{f}: pattern not found: {old[:80]}")
