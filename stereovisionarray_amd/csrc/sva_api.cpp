@@ -293,24 +293,54 @@ int run_sgm_batch(Ctx* c, const sva_pair_d* jobs, int n, int W, int H, size_t pi
     SVA_HIP(c, c->paths.ensure(nv * 4 * n), "path workspace");
     SVA_HIP(c, c->ckpt.ensure(ckb * n), "checkpoint workspace");
     uint8_t* C = (uint8_t*)c->cost.ptr;
-    for (int i = 0; i < n; i++) {
+    // The frames' census + cost kernels are VALU-bound and small: they run
+    // concurrently on up to tune::kBatchCostStreams side streams, forked from
+    // and joined back into the context stream.
+    const int ns = std::min(n, tune::kBatchCostStreams);
+    if (ns > 1) {
+        while ((int)c->side.size() < ns) {
+            hipStream_t s = nullptr;
+            hipEvent_t e = nullptr;
+            SVA_HIP(c, hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "side stream");
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+                (void)hipStreamDestroy(s);
+                return fail(c, SVA_ERR_DEVICE, "side stream event");
+            }
+            c->side.push_back(s);
+            c->side_done.push_back(e);
+        }
+        if (!c->fork) SVA_HIP(c, hipEventCreateWithFlags(&c->fork, hipEventDisableTiming), "fork event");
+        SVA_HIP(c, hipEventRecord(c->fork, c->stream), "fork");
+        for (int s = 0; s < ns; s++) SVA_HIP(c, hipStreamWaitEvent(c->side[s], c->fork, 0), "fork");
+    }
+    SVA_HIP(c, c->census_side.ensure(np * 16 * (size_t)ns), "census workspace");
+    const hipStream_t own = c->stream;
+    int st = SVA_OK;
+    for (int i = 0; i < n && st == SVA_OK; i++) {
         const sva_sgm_params* q = &jobs[i].params;
         uint8_t* Ci = C + (size_t)i * nv;
+        if (ns > 1) c->stream = c->side[i % ns];
+        hipError_t e;
         if (q->dir_y == 0 && Dp >= 128 && census_cost_supported(Dp)) {
-            SVA_HIP(c, launch_census_cost(*c, jobs[i].left, jobs[i].right, W, H, pitch, Dp, q->dmin,
-                                          q->dir, Ci, q->D),
-                    "cost launch");
+            e = launch_census_cost(*c, jobs[i].left, jobs[i].right, W, H, pitch, Dp, q->dmin, q->dir,
+                                   Ci, q->D);
         } else {
-            SVA_HIP(c, c->census_l.ensure(np * 8), "census workspace");
-            SVA_HIP(c, c->census_r.ensure(np * 8), "census workspace");
-            uint64_t* cl = (uint64_t*)c->census_l.ptr;
-            uint64_t* cr = (uint64_t*)c->census_r.ptr;
-            SVA_HIP(c, launch_census_pair(*c, jobs[i].left, jobs[i].right, W, H, pitch, cl, cr),
-                    "census launch");
-            SVA_HIP(c, launch_cost2(*c, cl, cr, W, H, Dp, q->dmin, q->dir, q->dir_y, Ci, q->D),
-                    "cost launch");
+            uint64_t* cl = (uint64_t*)c->census_side.ptr + (size_t)(i % ns) * 2 * np;
+            uint64_t* cr = cl + np;
+            e = launch_census_pair(*c, jobs[i].left, jobs[i].right, W, H, pitch, cl, cr);
+            if (e == hipSuccess)
+                e = launch_cost2(*c, cl, cr, W, H, Dp, q->dmin, q->dir, q->dir_y, Ci, q->D);
+        }
+        c->stream = own;
+        if (e != hipSuccess) st = hip_fail(c, e, "cost launch");
+    }
+    if (ns > 1) {   // join, also after a failed launch: the side streams stay ordered
+        for (int s = 0; s < ns; s++) {
+            SVA_HIP(c, hipEventRecord(c->side_done[s], c->side[s]), "join");
+            SVA_HIP(c, hipStreamWaitEvent(c->stream, c->side_done[s], 0), "join");
         }
     }
+    if (st) return st;
     uint8_t* L4 = (uint8_t*)c->paths.ptr;
     uint8_t* CK = (uint8_t*)c->ckpt.ptr;
     // horizontal planes of all frames, then vertical planes of all frames
@@ -471,6 +501,13 @@ int sva_destroy(void* ctx) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->batch_lane.reset();   // its streams and staging (multi.cpp), before the context's own
+    for (hipStream_t s : c->side) {
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamDestroy(s);
+    }
+    for (hipEvent_t e : c->side_done) (void)hipEventDestroy(e);
+    if (c->fork) (void)hipEventDestroy(c->fork);
+    c->census_side.release();
     for (DevBuf* b : {&c->census_l, &c->census_r, &c->cost, &c->paths, &c->ckpt, &c->scratch_u16,
                       &c->disp_r, &c->in_a, &c->in_b, &c->in_mask, &c->out_a, &c->out_b,
                       &c->out_c, &c->in_c, &c->shifted, &c->keys, &c->counts, &c->total})

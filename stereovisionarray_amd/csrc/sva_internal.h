@@ -67,6 +67,12 @@ struct Ctx {
     // sva_batch_sgm's per-context pipeline (copy streams, events, pinned and
     // device staging), created on first use and kept for later calls
     std::shared_ptr<void> batch_lane;
+    // sva_disparity_sgm_batch_d: side streams for the frames' census + cost
+    // (fork / join through events on `stream`), their census workspaces
+    std::vector<hipStream_t> side;
+    std::vector<hipEvent_t> side_done;
+    hipEvent_t fork = nullptr;
+    DevBuf census_side;
 };
 
 // Which launches a timing mode records: SVA_TIMING_ALL every one,

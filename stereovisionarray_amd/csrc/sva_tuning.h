@@ -101,6 +101,11 @@ constexpr int kWtahvSubLds = 1;
 // Frames per sgm_paths / wta_hv launch, and the workspace those frames may
 // hold (cost + 4 diagonal volumes + checkpoints per frame).
 constexpr int kBatchMaxPairs = 8;
+// Side streams for the batch's per-frame census + cost kernels (small and
+// VALU-bound at the reference's half-size frames: one after another on the
+// context stream they were 36 % of a 960x540 D=64 center8 step,
+// profiles/r04_*/c8half_batch.log.txt).
+constexpr int kBatchCostStreams = 3;
 constexpr size_t kBatchMaxBytes = (size_t)24 << 30;
 
 // ---- census.hip / census_cost.hip / cost.hip ------------
