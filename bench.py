@@ -79,6 +79,9 @@ def parse():
                          "rank 0 at N=1 and falls back to the committed profiles/pmc_*.json "
                          "if they fail; 'committed' reads the committed file only")
     ap.add_argument("--cpu-threads", type=int, default=1)
+    ap.add_argument("--mode-r-only", action="store_true",
+                    help="run only three GPU Mode R frames (1080p pair 12->11, k=20) and exit: "
+                         "the child of the Mode R VALU counter pass")
     ap.add_argument("--streams", type=int, default=0,
                     help="pairs of a step go round-robin to this many contexts, each with its "
                          "own HIP stream and workspaces, so pairs overlap (0 = auto: 2 when a "
@@ -177,11 +180,15 @@ def mode_r_beside(ctx, W, H, rows=24, k=20, reps=3):
                                       0.5, 1.0, d8.data_ptr())
     run()
     torch.cuda.synchronize()
+    ctx.set_timing(1)
+    ctx.reset_timing()
     t0 = time.perf_counter()
     for _ in range(reps):
         run()
     torch.cuda.synchronize()
     gdt = (time.perf_counter() - t0) / reps
+    km, kn = ctx.kernel_time("ref_match")
+    ctx.set_timing(0)
     mask = np.zeros((H, W), np.uint8)
     mask[H // 2 - rows // 2: H // 2 + rows // 2, :] = 1
     t0 = time.perf_counter()
@@ -190,10 +197,56 @@ def mode_r_beside(ctx, W, H, rows=24, k=20, reps=3):
     cdt = time.perf_counter() - t0
     g, c = n_cand / gdt / 1e6, ncpu / cdt / 1e6
     return {"unit": "Mcandidate-SADs/s", "gpu": round(g, 1), "gpu_ms_per_frame": round(gdt * 1e3, 3),
+            "ref_match_kernel_ms": round(km / kn, 4) if kn else None,
             "cpu": round(c, 3), "cores": 1, "kind": "port",
             "sample": f"oracle/refpath_oracle.c svo_ref_pair, {W}x{H} pair 12->11 k={k}: "
                       f"{rows} rows, {ncpu} candidates, {cdt:.2f} s",
             "gpu_over_cpu": round(g / c, 1)}
+
+
+def mode_r_only():
+    """Three GPU Mode R frames of mode_r_beside's workload (the PMC child)."""
+    import torch
+    import stereovisionarray_amd as sva
+    from stereovisionarray_amd import synth
+    W, H, k = 1920, 1080, 20
+    cams = synth.reference_array(0.036 / W)
+    cr, co = sva.Camera.make(*cams[12]), sva.Camera.make(*cams[11])
+    ref = synth.texture(H, W, 5)
+    oth = np.roll(ref, int(round(0.05 * 0.05 / 0.75 / (0.036 / W))), axis=1)
+    dev = torch.device("cuda", 0)
+    d_ref, d_oth = torch.from_numpy(ref).to(dev), torch.from_numpy(oth).to(dev)
+    d8 = torch.zeros((H, W), dtype=torch.uint8, device=dev)
+    ctx = sva.Context(0)
+    for _ in range(3):
+        ctx.disparity_ref_d(d_ref.data_ptr(), d_oth.data_ptr(), W, H, W, None, cr, co, k, 0.5, 1.0,
+                            d8.data_ptr())
+    torch.cuda.synchronize()
+    ctx.close()
+
+
+def mode_r_roofline(mr):
+    """Mode R is VALU/latency-bound, so its roofline is the
+    VALU issue rate: SQ_INSTS_VALU x 4 cycles (one wave64 VALU instruction
+    occupies a SIMD for 4 cycles) / (1,024 SIMDs x clock x kernel time), the
+    instructions from one live rocprofv3 pass over mode_r_only(), the kernel
+    time from the hipEvent-timed ref_match launches of mode_r_beside."""
+    import tempfile
+    outdir = tempfile.mkdtemp(prefix="sva_pmc_r_", dir="/tmp")
+    res = _pmc_pass("SQ_INSTS_VALU GRBM_GUI_ACTIVE", [], outdir, child=["--mode-r-only"])
+    c = res.get("ref_match", {})
+    insts = c.get("SQ_INSTS_VALU")
+    t_ms = mr.get("ref_match_kernel_ms")
+    if not insts or not t_ms:
+        raise RuntimeError("no ref_plane3_kernel counters")
+    cap = SIMDS * MI355X_ENGINE_GHZ * 1e9 * t_ms * 1e-3 / 4.0   # wave-instructions
+    return {"bound": "valu", "unit": "wave-instructions", "kernel": "ref_plane3_kernel<20>",
+            "sq_insts_valu": int(insts), "kernel_ms": t_ms,
+            "achieved_per_s": round(insts / (t_ms * 1e-3), 1),
+            "peak_per_s": round(SIMDS * MI355X_ENGINE_GHZ * 1e9 / 4.0, 1),
+            "frac": round(insts / cap, 4),
+            "grbm_gui_active": int(c.get("GRBM_GUI_ACTIVE", 0)),
+            "model": "SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x 2.4 GHz x ref_match time)"}
 
 
 def frame_overlap_beside(W, H, D, frames=40, rounds=2):
@@ -270,21 +323,26 @@ def committed_traffic(workload):
 
 # rocprofv3 kernel names -> bench timer names (the PMC pass reports per kernel)
 PMC_KERNELS = {"sgm_paths_kernel": "sgm_paths", "wta_hv_kernel": "wta_hv",
-               "census_cost_kernel": "cost"}
+               "census_cost_kernel": "cost", "ref_plane3_kernel": "ref_match"}
+MI355X_ENGINE_GHZ = 2.4   # peak engine clock (MI355X_MICROARCH.md)
+SIMDS = 1024              # 256 CUs x 4 SIMDs
 
 
-def _pmc_pass(counter, args, outdir):
-    """One rocprofv3 PMC pass (one counter, kernel trace only) over a short run of
-    this bench as a CHILD process; returns {timer name: mean counter per launch}."""
+def _pmc_pass(counter, args, outdir, child=None):
+    """One rocprofv3 PMC pass (one counter group, kernel trace only) over a short
+    run of this bench as a CHILD process; returns {timer name: mean counter per
+    launch} (several counters: {timer name: {counter: mean}})."""
     import csv
     import shutil
     import subprocess
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
-    d = os.path.join(outdir, counter.lower())
-    cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", counter, "--kernel-trace",
+    counters = counter.split()
+    d = os.path.join(outdir, counters[0].lower())
+    child = child if child is not None else ["--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+                                             "--pmc", "committed", "--streams", "1"] + args
+    cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc"] + counters + ["--kernel-trace",
            "-d", d, "-o", "run", "--output-format", "csv", "--",
-           sys.executable, os.path.abspath(__file__), "--steps", "3", "--warmup", "1",
-           "--no-cpu-baseline", "--pmc", "committed", "--streams", "1"] + args
+           sys.executable, os.path.abspath(__file__)] + child
     env = dict(os.environ, TMPDIR="/tmp", SVA_BENCH_PMC_CHILD="1")
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=170)
     if r.returncode != 0:
@@ -295,9 +353,14 @@ def _pmc_pass(counter, args, outdir):
         name = row["Kernel_Name"]
         for key, short in PMC_KERNELS.items():
             if key + "<" in name or key + "(" in name:
-                agg.setdefault(short, []).append(float(row["Counter_Value"]))
+                agg.setdefault((short, row["Counter_Name"]), []).append(float(row["Counter_Value"]))
                 break
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+    if len(counters) == 1:
+        return {k: sum(v) / len(v) for (k, _), v in agg.items()}
+    out = {}
+    for (k, c), v in agg.items():
+        out.setdefault(k, {})[c] = sum(v) / len(v)
+    return out
 
 
 def live_traffic(a):
@@ -1015,6 +1078,8 @@ def main():
 
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
+    if a.mode_r_only:
+        return mode_r_only()
     if mode == "engine":
         return run_engine(a, WORKLOADS[a.workload])
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -1203,6 +1268,13 @@ def main():
             out["cpu_baseline_all_cores"] = cpu_baseline(W, H, D, budget)
         # the reference's own CPU path (Mode R) timed beside its GPU port
         out["mode_r"] = mode_r_beside(ctx, W, H)
+        under_prof = any(k.startswith("ROCPROF") for k in os.environ) or \
+            os.environ.get("SVA_BENCH_PMC_CHILD")
+        if a.pmc == "live" and not under_prof:
+            try:
+                out["mode_r"]["roofline"] = mode_r_roofline(out["mode_r"])
+            except Exception as e:                  # keep the bench line; say why
+                out["mode_r"]["roofline"] = {"error": str(e)[:200]}
         if a.workload == "1080p_d128":
             out["frame_overlap"] = frame_overlap_beside(W, H, D)
     if rank == 0:

@@ -102,6 +102,22 @@ def test_aggregation_roofline(bench, monkeypatch):
     assert out["aggregation_roofline"]["traffic"] == 7
 
 
+def test_mode_r_valu_roofline(bench, monkeypatch):
+    """VERDICT r03 next #5: SQ_INSTS_VALU x 4 / (1024 SIMDs x 2.4 GHz x kernel time)."""
+    seen = {}
+
+    def fake(counter, args, outdir, child=None):
+        seen["counter"], seen["child"] = counter, child
+        return {"ref_match": {"SQ_INSTS_VALU": 300e6, "GRBM_GUI_ACTIVE": 2.0e6}}
+    monkeypatch.setattr(bench, "_pmc_pass", fake)
+    rf = bench.mode_r_roofline({"ref_match_kernel_ms": 0.8})
+    assert seen["counter"] == "SQ_INSTS_VALU GRBM_GUI_ACTIVE" and seen["child"] == ["--mode-r-only"]
+    assert abs(rf["frac"] - 300e6 * 4 / (1024 * 2.4e9 * 0.8e-3)) < 1e-4
+    assert rf["bound"] == "valu" and rf["sq_insts_valu"] == 300000000
+    with pytest.raises(RuntimeError):
+        bench.mode_r_roofline({"ref_match_kernel_ms": None})
+
+
 def mode_args(**kw):
     d = dict(gpus=1, engine="auto", rehearse_rccl=False, rehearse_overlap=False,
              dist_backend="nccl")
