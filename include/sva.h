@@ -174,15 +174,20 @@ int sva_paths_d(void* ctx, const uint8_t* C, int width, int height, const sva_sg
                 uint8_t* L8);
 int sva_aggregate_d(void* ctx, const uint8_t* C, int width, int height,
                     const sva_sgm_params* p, uint16_t* S);
-/* The two stages of the frame route, the tile pipeline.
- *   sva_paths_tile_d: diag = [4][H][W][D] u8, the volumes of directions 4..7
- *     (slot r - 4; same values as slots 4..7 of sva_paths_d); hckpt =
- *     [2][H][nsx][D] u8, hckpt[0][y][s] = L_0(s*seg + seg - 1, y) and
- *     hckpt[1][y][s] = L_1(s*seg, y); vckpt = [2][nsy][W][D] u8, vckpt[0][s][x]
- *     = L_2(x, s*seg + seg - 1) and vckpt[1][s][x] = L_3(x, s*seg) (entries
- *     with no such column / row are not written).
- *   sva_wta_hv_d: recomputes directions 0..3 per 16 x seg tile from the
- *     checkpoints, sums S with the diagonal volumes, picks d* (+ sub-pixel).
+/* The two stages of the frame route, the tile pipeline (DESIGN.md §4.9,
+ * §4.11).
+ *   sva_paths_tile_d: diag = [diag_volumes][H][W][D] u8, the diagonal
+ *     volumes (diag_volumes = 4 in this build: directions 4..7, the values of
+ *     those slots of sva_paths_d); hckpt = [2][H][nsx][D] u8, hckpt[0][y][s]
+ *     = L_0(s*seg + seg - 1, y) and hckpt[1][y][s] = L_1(s*seg, y); vckpt =
+ *     [6 - diag_volumes][nsy][W][D] u8, vckpt[0][s][x] = L_2(x, s*seg + seg
+ *     - 1), vckpt[1][s][x] = L_3(x, s*seg) (entries with no such column / row
+ *     are not written).  Experiment builds that recompute diagonals per tile
+ *     (measured slower and not shipped) report
+ *     diag_volumes 2 or 0 and carry those diagonals' row checkpoints in
+ *     vckpt planes 2.. instead; size every buffer from sva_tile_layout_of.
+ *   sva_wta_hv_d: recomputes the checkpointed directions per 16 x seg tile,
+ *     sums S with the diagonal volumes, picks d* (+ sub-pixel).
  * Every buffer comes with its size in bytes: a buffer smaller than its plane
  * returns SVA_ERR_INVALID_ARG before anything is launched.  seg, nsx, nsy and
  * the plane sizes come from sva_tile_layout_of (no device needed);
@@ -190,10 +195,11 @@ int sva_aggregate_d(void* ctx, const uint8_t* C, int width, int height,
 typedef struct sva_tile_layout {
     int32_t seg;          /* checkpoint spacing, columns and rows            */
     int32_t nsx, nsy;     /* ceil(W / seg), ceil(H / seg)                    */
+    int32_t diag_volumes; /* 4: directions 4..7 (2 or 0: §4.11 builds)     */
     size_t cost_bytes;    /* C      [H][W][D]                                */
-    size_t diag_bytes;    /* diag   [4][H][W][D]                             */
+    size_t diag_bytes;    /* diag   [diag_volumes][H][W][D]                  */
     size_t hckpt_bytes;   /* hckpt  [2][H][nsx][D]                           */
-    size_t vckpt_bytes;   /* vckpt  [2][nsy][W][D]                           */
+    size_t vckpt_bytes;   /* vckpt  [6 - diag_volumes][nsy][W][D]            */
 } sva_tile_layout;
 int sva_tile_layout_of(int width, int height, int D, sva_tile_layout* out);
 int sva_tile_check(int width, int height, int D, size_t C_bytes, size_t diag_bytes,

@@ -87,6 +87,7 @@ class Camera(ct.Structure):
 class TileLayout(ct.Structure):
     """Mirror of ``sva_tile_layout`` (include/sva.h): the tile stages' buffers."""
     _fields_ = [("seg", ct.c_int32), ("nsx", ct.c_int32), ("nsy", ct.c_int32),
+                ("diag_volumes", ct.c_int32),
                 ("cost_bytes", ct.c_size_t), ("diag_bytes", ct.c_size_t),
                 ("hckpt_bytes", ct.c_size_t), ("vckpt_bytes", ct.c_size_t)]
 

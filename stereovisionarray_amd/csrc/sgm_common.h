@@ -260,10 +260,10 @@ template <int DPL> constexpr int pf_v() {
 
 
 // One path line over a materialised cost volume C.  CKPT
-// 1 (horizontal lines) / 2 (vertical lines): store checkpoints every 2^SL
-// pixels to rCK instead of the full L_r line to rL (SL is a template
-// parameter: a runtime segment test cost the latency-bound lines of small
-// frames 20 %).
+// 1 (horizontal lines) / 2 (vertical lines) / 3 (down-diagonal lines): store
+// checkpoints every 2^SL pixels (rows for 2 and 3) to rCK instead of the full
+// L_r line to rL (SL is a template parameter: a runtime segment test cost the
+// latency-bound lines of small frames 20 %).
 template <int DPL, bool DIAG, int PF, int CKPT = 0, int SL = 0>
 __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& g, int rx, int ry,
                                           int line, int k, rsrc_t rCK) {
@@ -345,6 +345,19 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
             if (hit)   // default policy (tune::kCkptStoreAux): the WTA kernel reads these back soon
                 bstore<NW, tune::kCkptStoreAux>(rCK, ((unsigned)(y0 * g.ns + (x >> SL)) * (unsigned)D +
                                          (unsigned)(k * DPL)), ow);
+        } else if constexpr (CKPT == 3) {
+            // diagonal line with row checkpoints: a down
+            // line (ry = +1) keeps the last row of every row segment but the
+            // image's last, an up line (ry = -1) the first row of every
+            // segment but the first, in the row checkpoint plane [nsy][W][D]
+            // at this pixel's column: the pixel's volume offset minus the
+            // rows the plane does not hold
+            const int y = ry > 0 ? ts : H - 1 - ts;
+            constexpr int SEG = 1 << SL;
+            const bool hit = ry > 0 ? (((y + 1) & (SEG - 1)) == 0 && y + 1 < H)
+                                    : ((y & (SEG - 1)) == 0 && y > 0);
+            if (hit)
+                bstore<NW, tune::kCkptStoreAux>(rCK, cc.off - (unsigned)(y - (y >> SL)) * WD, ow);
         } else if constexpr (CKPT == 2) {
             // vertical line x0: direction 2 (down) keeps the last row of every
             // row segment but the column's last, direction 3 (up) the first row

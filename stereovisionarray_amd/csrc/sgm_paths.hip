@@ -27,12 +27,13 @@
 // Two output modes (g.ckpt):
 //   0  every direction writes its u8 volume, [8][H][W][D] (sva_paths_d, the
 //      stage API the parity tests read): 8 C reads + 8 L writes per disparity.
-//   2  the frame route, the tile pipeline: only the four
-//      diagonal directions write volumes, [4][H][W][D] (direction r at slot
-//      r - 4); horizontal lines store checkpoints every seg columns
-//      ([2][H][nsx][D]), vertical lines every seg rows ([2][nsy][W][D]; seg =
-//      2^tile_geom().seg_log2), and wta_hv.hip recomputes all four per tile:
-//      8 C reads + 4 L writes.
+//   2  the frame route, the tile pipeline: the up
+//      diagonals 5 and 7 write volumes, [2][H][W][D] (slots 0, 1); horizontal
+//      lines store checkpoints every seg columns ([2][H][nsx][D]), vertical
+//      and down-diagonal lines every seg rows ([4][nsy][W][D]: directions 2,
+//      3, 4, 6; seg = 2^tile_geom().seg_log2), and wta_hv.hip recomputes
+//      those six per tile: 8 C reads + 2 L writes.  (tune::kTileDiagDown =
+//      0: all four diagonals write volumes, [4][H][W][D], round 3.)
 //   (Mode 1, the round-2 route of DESIGN.md §4.6 -- six volumes, horizontal
 //   checkpoints only, finished by wta_h.hip -- was removed in ABI v5.)
 #include "sgm_common.h"
@@ -91,17 +92,30 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
     int rx, ry;
     dir_of(r, rx, ry);
     const rsrc_t rC = make_rsrc(C, g.vol);
-    const int slot = g.ckpt ? r - 4 : r;
     // the tile pipeline's checkpoint segment (§4.9), rows and columns
     constexpr int SL = DPL <= 8 ? tune::kWtahvTileLog2 : tune::kWtahvTileLog2Wide;
-    if (r >= 4) {
+    constexpr bool DOWN = tune::kTileDiagDown != 0, UP = tune::kTileDiagUp != 0;
+    if (r >= 4 && g.ckpt && (ry > 0 ? DOWN : UP)) {
+        // tile pipeline, diagonals recomputed per tile: row
+        // checkpoints only, in the vertical checkpoint block after the two
+        // vertical planes: the down pair (4, 6), then the up pair (5, 7)
+        const int plane = ry > 0 ? 2 + (r == 4 ? 0 : 1) : 2 + (DOWN ? 2 : 0) + (r == 5 ? 0 : 1);
+        const rsrc_t rCK = make_rsrc(CKV + (size_t)plane * g.ckvvol, g.ckvvol);
+        path_line<DPL, true, pf_v<DPL>(), 3, SL>(rC, rC, g, rx, ry, line, k, rCK);
+    } else if (r >= 4) {
+        // volume slot: every direction (8 volumes), or the tile pipeline's
+        // diagonals that stay volumes, in direction order
+        const int slot = !g.ckpt ? r
+                       : DOWN ? (r == 5 ? 0 : 1)          // 5, 7 (UP is then off here)
+                       : UP ? (r == 4 ? 0 : 1)            // 4, 6
+                       : r - 4;
         const rsrc_t rL = make_rsrc(L8 + (size_t)slot * g.vol, g.vol);
         path_line<DPL, true, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
     } else if (r >= 2 && g.ckpt) {
         const rsrc_t rCK = make_rsrc(CKV + (size_t)(r - 2) * g.ckvvol, g.ckvvol);
         path_line<DPL, false, pf_v<DPL>(), 2, SL>(rC, rC, g, rx, ry, line, k, rCK);
     } else if (r >= 2) {
-        const rsrc_t rL = make_rsrc(L8 + (size_t)slot * g.vol, g.vol);
+        const rsrc_t rL = make_rsrc(L8 + (size_t)r * g.vol, g.vol);
         path_line<DPL, false, pf_v<DPL>()>(rC, rL, g, rx, ry, line, k, rL);
     } else if (g.ckpt) {
         const rsrc_t rCK = make_rsrc(CK + (size_t)r * g.ckvol, g.ckvol);
@@ -125,6 +139,9 @@ TileGeom tile_geom(int W, int H, int D) {
     t.nsx = (W + seg - 1) >> t.seg_log2;
     t.hck_bytes = 2 * (size_t)H * t.nsx * D;
     t.vck_bytes = 2 * (size_t)t.nty * W * D;
+    const int ndp = (tune::kTileDiagDown ? 2 : 0) + (tune::kTileDiagUp ? 2 : 0);
+    t.dck_bytes = (size_t)ndp / 2 * t.vck_bytes;   // one plane per recomputed diagonal
+    t.nvol = 4 - ndp;
     return t;
 }
 
@@ -140,7 +157,7 @@ hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, i
     g.ckpt = CK ? 2 : 0;
     const TileGeom tg = tile_geom(W, H, D);
     g.nsy = tg.nty;
-    g.ckvvol = tg.vck_bytes / 2;
+    g.ckvvol = tg.vck_bytes / 2;        // one row-checkpoint plane
     g.ns = tg.nsx;
     g.ckvol = tg.hck_bytes / 2;
     if (g.vol >= (size_t)1 << 32) return hipErrorInvalidValue;  // 32-bit buffer offsets
@@ -148,9 +165,9 @@ hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, i
     if (npair < 1 || (npair > 1 && !CK)) return hipErrorInvalidValue;
     g.npair = npair;
     g.cstr = g.vol;
-    g.lstr = 4 * g.vol;
+    g.lstr = (size_t)tg.nvol * g.vol;
     g.ckstr = tg.hck_bytes;
-    g.ckvstr = tg.vck_bytes;
+    g.ckvstr = tg.vck_bytes + tg.dck_bytes;
     dim3 grid((unsigned)((2 * g.blk_h + 6 * g.blk_w) * npair));
 #define SVA_PATHS_LAUNCH(DPL_)                                                               \
     hipExtLaunchKernelGGL(sgm_paths_kernel<DPL_>, grid, dim3(PATH_BLOCK), 0, c.stream, t.start, \

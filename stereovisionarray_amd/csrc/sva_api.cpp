@@ -178,8 +178,8 @@ int paths_wta(Ctx* c, const uint8_t* C, int W, int H, const sva_sgm_params* p, i
     if (!wta_hv_supported(Dp)) return fail(c, SVA_ERR_UNSUPPORTED, "no tile pipeline for this D");
     const size_t nv = (size_t)W * H * (size_t)Dp;
     const TileGeom tg = tile_geom(W, H, Dp);
-    SVA_HIP(c, c->paths.ensure(nv * 4), "path workspace");
-    SVA_HIP(c, c->ckpt.ensure(tg.hck_bytes + tg.vck_bytes), "checkpoint workspace");
+    SVA_HIP(c, c->paths.ensure(nv * tg.nvol), "path workspace");
+    SVA_HIP(c, c->ckpt.ensure(tg.hck_bytes + tg.vck_bytes + tg.dck_bytes), "checkpoint workspace");
     uint8_t* L4 = (uint8_t*)c->paths.ptr;
     uint8_t* CK = (uint8_t*)c->ckpt.ptr;
     uint8_t* CKV = CK + tg.hck_bytes;
@@ -198,9 +198,10 @@ sva_tile_layout tile_layout(int W, int H, int D) {
     l.nsx = tg.nsx;
     l.nsy = tg.nty;
     l.cost_bytes = (size_t)W * H * (size_t)D;
-    l.diag_bytes = 4 * l.cost_bytes;
+    l.diag_volumes = tg.nvol;
+    l.diag_bytes = (size_t)tg.nvol * l.cost_bytes;
     l.hckpt_bytes = tg.hck_bytes;
-    l.vckpt_bytes = tg.vck_bytes;
+    l.vckpt_bytes = tg.vck_bytes + tg.dck_bytes;
     return l;
 }
 
@@ -211,14 +212,15 @@ int check_tile_buffers(Ctx* c, int W, int H, int D, const void* C, size_t C_byte
                        const void* diag, size_t diag_bytes, const void* hck, size_t hck_bytes,
                        const void* vck, size_t vck_bytes) {
     const sva_tile_layout l = tile_layout(W, H, D);
-    if (!C || !diag || !hck || !vck) return fail(c, SVA_ERR_INVALID_ARG, "null stage buffer");
+    if (!C || (!diag && l.diag_bytes) || !hck || !vck)
+        return fail(c, SVA_ERR_INVALID_ARG, "null stage buffer");
     if (C_bytes < l.cost_bytes) return fail(c, SVA_ERR_INVALID_ARG, "cost buffer smaller than [H][W][D]");
     if (diag_bytes < l.diag_bytes)
-        return fail(c, SVA_ERR_INVALID_ARG, "diagonal volume buffer smaller than [4][H][W][D]");
+        return fail(c, SVA_ERR_INVALID_ARG, "diagonal volume buffer smaller than [nvol][H][W][D]");
     if (hck_bytes < l.hckpt_bytes)
         return fail(c, SVA_ERR_INVALID_ARG, "horizontal checkpoint buffer smaller than [2][H][nsx][D]");
     if (vck_bytes < l.vckpt_bytes)
-        return fail(c, SVA_ERR_INVALID_ARG, "vertical checkpoint buffer smaller than [2][nsy][W][D]");
+        return fail(c, SVA_ERR_INVALID_ARG, "row checkpoint buffer smaller than [np][nsy][W][D]");
     return SVA_OK;
 }
 
@@ -288,9 +290,9 @@ int run_sgm_batch(Ctx* c, const sva_pair_d* jobs, int n, int W, int H, size_t pi
     const int Dp = padded_D(p->D);
     const size_t np = (size_t)W * H, nv = np * (size_t)Dp;
     const TileGeom tg = tile_geom(W, H, Dp);
-    const size_t ckb = tg.hck_bytes + tg.vck_bytes;
+    const size_t ckb = tg.hck_bytes + tg.vck_bytes + tg.dck_bytes;
     SVA_HIP(c, c->cost.ensure(nv * n), "cost workspace");
-    SVA_HIP(c, c->paths.ensure(nv * 4 * n), "path workspace");
+    SVA_HIP(c, c->paths.ensure(nv * tg.nvol * n), "path workspace");
     SVA_HIP(c, c->ckpt.ensure(ckb * n), "checkpoint workspace");
     uint8_t* C = (uint8_t*)c->cost.ptr;
     // The frames' census + cost kernels are VALU-bound and small: they run
@@ -547,9 +549,9 @@ int sva_reserve(void* ctx, int W, int H, int D) {
     SVA_HIP(c, c->census_r.ensure(np * 8), "reserve");
     SVA_HIP(c, c->cost.ensure(nv), "reserve");
     // the frame route's path volumes: the 4 diagonal directions (tile pipeline)
-    SVA_HIP(c, c->paths.ensure(nv * 4), "reserve");
+    SVA_HIP(c, c->paths.ensure(nv * tile_geom(W, H, D).nvol), "reserve");
     const TileGeom tg = tile_geom(W, H, D);
-    SVA_HIP(c, c->ckpt.ensure(tg.hck_bytes + tg.vck_bytes), "reserve");
+    SVA_HIP(c, c->ckpt.ensure(tg.hck_bytes + tg.vck_bytes + tg.dck_bytes), "reserve");
     return SVA_OK;
 }
 
@@ -632,7 +634,8 @@ int sva_disparity_sgm_batch_d(void* ctx, const sva_pair_d* jobs, int n, int W, i
     // under tune::kBatchMaxBytes
     const int Dp = padded_D(p0->D);
     const TileGeom tg = tile_geom(W, H, Dp);
-    const size_t per = (size_t)W * H * (size_t)Dp * 5 + tg.hck_bytes + tg.vck_bytes;
+    const size_t per = (size_t)W * H * (size_t)Dp * (1 + tg.nvol) + tg.hck_bytes + tg.vck_bytes +
+                       tg.dck_bytes;
     int chunk = tune::kBatchMaxPairs;
     while (chunk > 1 && per * (size_t)chunk > tune::kBatchMaxBytes) chunk--;
     const size_t np = (size_t)W * H;

@@ -143,11 +143,12 @@ hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right,
 hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,
                        int dmin, int dir, uint8_t* C, int dreal = 0);
 // sgm_paths.hip -- all 8 directions in one launch.  CK == CKV == nullptr:
-// L8 = [8][H][W][D] u8.  CK and CKV set (the tile pipeline):
-// L8 = [4][H][W][D] (directions 4..7), CK = [2][H][nsx][D] and CKV =
-// [2][nsy][W][D] (tile_geom below).  npair > 1 (tile pipeline only): a batch
-// of frames in one launch, each buffer holding npair such planes back to back
-// (DESIGN.md §4.10).
+// L8 = [8][H][W][D] u8.  CK and CKV set (the tile pipeline, DESIGN.md §4.9,
+// §4.11): L8 = [nvol][H][W][D] (directions 5, 7, or 4..7), CK = [2][H][nsx][D]
+// and CKV = the vertical then the down-diagonal row checkpoints,
+// vck_bytes + dck_bytes (tile_geom below).  npair > 1 (tile pipeline only): a
+// batch of frames in one launch, each buffer holding npair such planes back
+// to back.
 hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
                         uint8_t* L8, uint8_t* CK = nullptr, uint8_t* CKV = nullptr,
                         int npair = 1);
@@ -159,7 +160,9 @@ struct TileGeom {
     int ntx, nty;             // tiles per row / per column (nty = vertical segments)
     int nsx;                  // horizontal segments per row
     size_t hck_bytes;         // [2][H][nsx][D]
-    size_t vck_bytes;         // [2][nty][W][D]
+    size_t vck_bytes;         // [2][nty][W][D]: directions 2, 3
+    size_t dck_bytes;         // [2][nty][W][D]: directions 4, 6 (0 when they are volumes)
+    int nvol;                 // diagonal volumes the path kernel writes: 2 (5, 7) or 4
 };
 TileGeom tile_geom(int W, int H, int D);
 bool paths_supported(int D);

@@ -44,6 +44,17 @@ constexpr int kCkptStoreAux = 0;
 constexpr int kStateMinTree = 1;
 
 // ---- wta_hv.hip -------------------------------------------
+// The down diagonals (directions 4 and 6) recomputed per tile from row
+// checkpoints with a 7-column halo (1), or written as volumes by sgm_paths
+// and read back (0).  The up diagonals (5 and 7) likewise,
+// from the checkpoint row below the tile.  Both 0: the recompute moves
+// sgm_paths' saved bytes into VALU on the VALU-bound wta_hv.  Frame ms,
+// none / down pair / all four, in-process A/B with equal maps
+// (profiles/r04_v3/ab_diag_recompute.log.txt): 1080p D=128 0.891 / 0.936 /
+// 1.010, D=192 1.324 / 1.355 / 1.367, D=256 1.735 / 1.836 / 1.931, 4K D=128
+// 3.772 / 3.863 / 3.944, 4K D=256 7.570 / 7.394 / 7.697.
+constexpr int kTileDiagDown = 0;
+constexpr int kTileDiagUp = 0;
 // log2 of the tile rows and of the checkpoint segment (tiles are 16 x 2^this).
 constexpr int kWtahvTileLog2 = 3;
 constexpr int kWtahvTileLog2Wide = 3;      // D > 128
@@ -96,6 +107,17 @@ constexpr int kWtahvPinWta = 1;
 // -> 0.2495 / 0.2450 ms, D=64 0.150 -> 0.144, D=192 0.393 -> 0.380, D=256
 // 0.556 -> 0.538, 4K D=256 2.215 -> 2.158.
 constexpr int kWtahvSubLds = 1;
+// LDS V blocks at D = 256 (8 u16 pairs = two 16-byte chunks per lane): 1 swaps
+// a lane's two chunks when ((k >> 2) ^ (k >> 3)) & 1, which makes every
+// ds_write_b128 (8-lane groups, 32 banks) and ds_read_b128 (16-lane groups
+// spanning two slot rows, 64 banks) of the block conflict-free; 0 keeps the
+// plain [lane][pair] order (2-way conflicts on both).  0: the swizzle cut
+// wta_hv's bank-conflict cycles 20.9 M -> 1.6 M and its LDS-active cycles
+// 42.0 M -> 22.6 M per 1080p D=256 launch, but the kernel is VALU-bound and
+// the two lane bases cost registers (190 -> 197 VGPRs): wta_hv 0.5097 ->
+// 0.5223 ms at 1080p D=256, 2.065 -> 2.108 ms at 4K D=256; D=128 / 192
+// unchanged (profiles/r04_v3/ab_vswizzle.log.txt, pmc_vswizzle.txt).
+constexpr int kWtahvVSwizzle = 0;
 
 // ---- batched frames (sva_disparity_sgm_batch_d) ----------
 // Frames per sgm_paths / wta_hv launch, and the workspace those frames may

@@ -73,10 +73,14 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
     const unsigned tb = blockIdx.x - f * (unsigned)g.tiles;
     const int tx = (int)(tb % (unsigned)g.ntx);
     const int ty = (int)(tb / (unsigned)g.ntx);
+    // diagonals recomputed per tile (§4.11): the down pair (4, 6), the up pair (5, 7)
+    constexpr bool DOWN = tune::kTileDiagDown != 0, UP = tune::kTileDiagUp != 0;
+    constexpr int ND = (DOWN ? 2 : 0) + (UP ? 2 : 0);   // recomputed diagonals
+    constexpr int NV = 4 - ND;                          // diagonal volumes read
     C += (size_t)f * g.vol;
-    L4 += (size_t)f * 4 * g.vol;
+    L4 += (size_t)f * NV * g.vol;
     CK += (size_t)f * 2 * g.hck;
-    CKV += (size_t)f * 2 * g.vck;
+    CKV += (size_t)f * (2 + ND) * g.vck;
     disp += (size_t)f * (size_t)g.W * (size_t)g.H;
     if (sub) sub += (size_t)f * (size_t)g.W * (size_t)g.H;
     const int slot = (int)(threadIdx.x >> 4);
@@ -98,8 +102,15 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
     }
 
     // V = L_2 + L_3 per tile pixel, [pixel = r * TW + c][lane k][NP pairs]:
-    // each 16-lane row reads / writes 16 consecutive NP-dword chunks.
+    // each 16-lane row reads / writes 16 consecutive NP-dword chunks.  At
+    // NP = 8 a lane's two 16-byte chunks trade places when ((k >> 2) ^
+    // (k >> 3)) & 1 (tune::kWtahvVSwizzle): bank-conflict-free b128 reads and
+    // writes.  vw(p) = the word of pair p inside a pixel block.
     __shared__ unsigned vsum[TY * TW * 16 * NP];
+    constexpr bool VSW = NP == 8 && tune::kWtahvVSwizzle != 0;
+    auto vsw_of = [](int kk) -> int { return VSW ? (((kk >> 2) ^ (kk >> 3)) & 1) * 4 : 0; };
+    const int vb0 = k * NP + vsw_of(k), vb1 = k * NP + (4 ^ vsw_of(k));
+    auto vw = [&](int p) -> int { return (p < 4 ? vb0 : vb1) + (p & 3); };
 
     // phase V: column x0 + slot; phase H: row hr, columns [hx, hx + TY)
     const bool vcol = slot < nx;
@@ -164,9 +175,9 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
                 for (int q = 0; q < NW; q++) unpack4(ld[q], V[2 * q], V[2 * q + 1]);
                 unpack_add<NW>(lu, V);
             }
-            unsigned* dst = &vsum[((r * TW + slot) * 16 + k) * NP];
+            unsigned* dst = &vsum[(r * TW + slot) * 16 * NP];
 #pragma unroll
-            for (int p = 0; p < NP; p++) dst[p] = V[p];
+            for (int p = 0; p < NP; p++) dst[vw(p)] = V[p];
         };
         unsigned LD[TY][NK];
         if constexpr (tune::kWtahvInterleaveV != 0) {
@@ -205,20 +216,111 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
             });
         }
     }
+    if constexpr (ND > 0) {
+        // ---- phase D: diagonals recomputed per tile ------
+        // Direction 4 (+x) and 6 (-x) come down from the row checkpoint at
+        // y0 - 1, 5 (-x) and 7 (+x) up from the one at y0 + TY (zero state at
+        // the image's top / bottom edge).  Each has NL = 16 + TY - 1 lines
+        // crossing the tile; a line's first TY - 1 pixels can lie in the halo
+        // beside it.  In-tile pixels add L into V with LDS atomics (packed u16
+        // pairs: V + four diagonals <= 1530 per half, no carry), so every
+        // direction's runs share the slots in any order.  A line off the
+        // image restarts (zero state) like the path kernel's wrapped lines.
+        __syncthreads();                              // V stored before the adds
+        constexpr int NL = TW + TY - 1;
+        constexpr int NRUN = (ND * NL + 15) / 16;     // runs per slot
+        const rsrc_t rCKD = make_rsrc(CKV + 2 * (size_t)g.vck, (unsigned)ND * g.vck);
+        // run i of this slot: line q = slot + 16 i of the ND * NL
+        struct Run {
+            int c, rx, yck;   // column at the checkpoint row, x step, checkpoint segment
+            unsigned plane;   // its plane in rCKD
+            bool up, ok;
+        };
+        auto run_of = [&](int i) __attribute__((always_inline)) -> Run {
+            Run u;
+            const int q = slot + 16 * i;
+            const int dd = q / NL, li = q - dd * NL;
+            u.ok = q < ND * NL;
+            u.up = !DOWN || dd >= 2;
+            const int e = u.up && DOWN ? dd - 2 : dd;     // 0 or 1 within its pair
+            // down: 4 (+x), 6 (-x); up: 5 (-x), 7 (+x)
+            u.rx = u.up ? (e ? 1 : -1) : (e ? -1 : 1);
+            u.c = u.rx > 0 ? x0 - TY + li : x0 + 1 + li;
+            u.plane = (unsigned)dd;
+            u.yck = u.up ? (y0 + TY < H ? ty + 1 : -1) : ty - 1;   // -1: no checkpoint
+            return u;
+        };
+        auto issue_d = [&](int i, Words<NW>& ck, Words<NW> (&cd)[TY]) __attribute__((always_inline)) {
+            const Run u = run_of(i);
+            const bool ckin = u.yck >= 0 && (unsigned)u.c < (unsigned)W;
+            ck = bload<NW>(rCKD, ckin ? u.plane * g.vck + ((unsigned)u.yck * uW + (unsigned)u.c) * uD +
+                                            lane_d
+                                      : 0u);
+#pragma unroll
+            for (int s = 0; s < TY; s++) {
+                const int x = u.c + u.rx * (s + 1);
+                const int y = u.up ? y0 + TY - 1 - s : y0 + s;
+                cd[s] = bload<NW>(rC, (unsigned)x < (unsigned)W && y < H
+                                          ? ((unsigned)y * uW + (unsigned)x) * uD + lane_d
+                                          : 0u);
+            }
+        };
+        auto run_d = [&](int i, const Words<NW>& ck, const Words<NW> (&cd)[TY]) __attribute__((always_inline)) {
+            const Run u = run_of(i);
+            if (!u.ok) return;                        // uniform per 16-lane row
+            unsigned A[NP], m;
+            if (u.yck >= 0 && (unsigned)u.c < (unsigned)W) state_from_words<DPL, PAD, PIN>(ck, A, m, padm);
+            else zero_state(A, m);
+            for_seq<TY>([&](auto R) {
+                constexpr int s = decltype(R)::value;
+                const int x = u.c + u.rx * (s + 1);
+                const int r = u.up ? TY - 1 - s : s;      // tile row
+                if ((unsigned)x < (unsigned)W && r < ny) {
+                    unsigned ow[NW];
+                    sgm_step<DPL, PIN>(cd[s].w, A, m, ow, P1, P2, eb);
+                    if (x >= x0 && x < x0 + nx) {
+                        unsigned* dst = &vsum[(r * TW + (x - x0)) * 16 * NP];
+#pragma unroll
+                        for (int p = 0; p < NP; p++) atomicAdd(&dst[vw(p)], A[p]);
+                    }
+                } else {
+                    zero_state(A, m);                   // off the image: restart
+                }
+            });
+        };
+        if constexpr (DPL <= 8) {
+            // the next run's loads go out before this run's recurrence
+            Words<NW> ck[2], cd[2][TY];
+            issue_d(0, ck[0], cd[0]);
+            for_seq<NRUN>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                if constexpr (i + 1 < NRUN) issue_d(i + 1, ck[(i + 1) & 1], cd[(i + 1) & 1]);
+                run_d(i, ck[i & 1], cd[i & 1]);
+            });
+        } else {
+            Words<NW> ck, cd[TY];
+            for_seq<NRUN>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                issue_d(i, ck, cd);
+                run_d(i, ck, cd);
+            });
+        }
+    }
     if constexpr (tune::kWtahvRowCFirst == 0) load_row();
     // phase H's first global loads (checkpoints, diagonal volumes) go out
     // before the barrier (tune::kWtahvEarlyLoads)
     const int hs = hx >> TYL;                          // the row segment's index
     const unsigned ckrow = yh * (unsigned)g.nsx;
     Words<NW> ckw[2];
-    rsrc_t rV[4];
+    constexpr int NVA = NV > 0 ? NV : 1;               // (array extent; NV may be 0)
+    rsrc_t rV[NVA];
 #pragma unroll
-    for (int r = 0; r < 4; r++) rV[r] = make_rsrc(L4 + (size_t)r * g.vol, g.vol);
-    Words<NW> rv[kPfVol][4];
+    for (int r = 0; r < NV; r++) rV[r] = make_rsrc(L4 + (size_t)r * g.vol, g.vol);
+    Words<NW> rv[kPfVol][NVA];
     auto issue = [&](int s, int j) {
         const unsigned off = (yh * uW + (unsigned)(hx + j)) * uD + lane_d;
 #pragma unroll
-        for (int r = 0; r < 4; r++) rv[s][r] = bload<NW, 2>(rV[r], off);   // last use: nt
+        for (int r = 0; r < NV; r++) rv[s][r] = bload<NW, 2>(rV[r], off);   // last use: nt
     };
     auto issue_first = [&]() {
         // (words outside the image are never used: the first / last segment
@@ -261,10 +363,9 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
             unsigned ow[NW];
             sgm_step<DPL, PIN>(ch[j].w, Aa, ma, ow, P1, P2, ea);
             unsigned* const vpix = &vsum[(hr * TW + hseg * TY + j) * 16 * NP];   // this pixel's V
-            const unsigned* vs = vpix + k * NP;
             unsigned S[NP];
 #pragma unroll
-            for (int p = 0; p < NP; p++) S[p] = vs[p] + Aa[p];   // V + L_1
+            for (int p = 0; p < NP; p++) S[p] = vpix[vw(p)] + Aa[p];   // V + L_1
             if constexpr (KEEP16H) {
 #pragma unroll
                 for (int p = 0; p < NP; p++) S[p] += LF[j][p];     // + L_0
@@ -272,7 +373,7 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
                 unpack_add<NW>(LF[j], S);
             }
 #pragma unroll
-            for (int r = 0; r < 4; r++) unpack_add<NW>(rv[s][r].w, S);
+            for (int r = 0; r < NV; r++) unpack_add<NW>(rv[s][r].w, S);
             if constexpr (PAD) {
 #pragma unroll
                 for (int p = 0; p < NP; p++) S[p] |= padm[p];
@@ -281,13 +382,13 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
             if constexpr (tune::kWtahvSubLds != 0) {
                 // S(d*-1) and S(d*+1) through LDS: every lane writes its S
                 // pairs over the pixel's V block, which nothing reads again;
-                // as u16 the block is S indexed by d.  The owning lane reads
+                // as u16 the block is S indexed by d (up to the swizzle).  The owning lane reads
                 // the two neighbours (same wave, behind a wave barrier).
                 const unsigned best = wta_pick_key<DPL, PIN && tune::kWtahvPinWta>(S, k);
                 const int ds = (int)(best & 0xffffu);
                 if (want_sub) {
 #pragma unroll
-                    for (int p = 0; p < NP; p++) vpix[k * NP + p] = S[p];
+                    for (int p = 0; p < NP; p++) vpix[vw(p)] = S[p];
                     // the owning lane reads what other lanes of this wave just
                     // wrote: state the ordering (a wave's LDS operations
                     // execute in issue order, so this costs no instruction)
@@ -301,7 +402,12 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
                     if (want_sub) {
                         const uint16_t* s16 = reinterpret_cast<const uint16_t*>(vpix);
                         const int dm = ds > 0 ? ds - 1 : 0, dp = ds + 1 < 16 * DPL ? ds + 1 : ds;
-                        sm = (unsigned)s16[dm] | ((unsigned)s16[dp] << 16);
+                        // u16 of disparity d: pair (d / 2) % NP of lane d / DPL
+                        auto at = [&](int d) {
+                            const int kk = d / DPL, pp = (d >> 1) % NP;
+                            return (unsigned)s16[2 * (kk * NP + (pp ^ vsw_of(kk))) + (d & 1)];
+                        };
+                        sm = at(dm) | (at(dp) << 16);
                     }
                 }
             } else {

@@ -67,8 +67,10 @@ def test_tile_stage_sizes_checked_without_device(sva):
     W, H, D = 1920, 1080, 128
     lay = sva.tile_layout(W, H, D)
     assert (lay.seg, lay.nsx, lay.nsy) == (8, 240, 135)
-    assert lay.cost_bytes == W * H * D and lay.diag_bytes == 4 * W * H * D
-    assert lay.hckpt_bytes == 2 * H * 240 * D and lay.vckpt_bytes == 2 * 135 * W * D
+    nv = lay.diag_volumes
+    assert nv in (2, 4)
+    assert lay.cost_bytes == W * H * D and lay.diag_bytes == nv * W * H * D
+    assert lay.hckpt_bytes == 2 * H * 240 * D and lay.vckpt_bytes == (6 - nv) * 135 * W * D
     full = [lay.cost_bytes, lay.diag_bytes, lay.hckpt_bytes, lay.vckpt_bytes]
     assert sva.lib.sva_tile_check(W, H, D, *full) == sva.SVA_OK
     for i in range(4):

@@ -1,9 +1,12 @@
-"""The frame route's two stages (the tile pipeline) through
-their ABI v5 entry points, against the CPU oracle, bit-exact:
-sva_paths_tile_d writes the four diagonal volumes (directions 4..7) and the
-horizontal / vertical checkpoints (the oracle's L_0 / L_1 at the checkpoint
-columns, L_2 / L_3 at the checkpoint rows); sva_wta_hv_d recomputes the other
-four directions per tile and picks d* (sub-pixel within 1e-5 px, observed 0).
+"""The frame route's two stages (the tile pipeline)
+through their ABI v5 entry points, against the CPU oracle, bit-exact:
+sva_paths_tile_d writes the diagonal volumes and the checkpoints (the
+oracle's L_0 / L_1 at the checkpoint columns, L_2 / L_3 at the checkpoint
+rows, and in a build that recomputes the down diagonals per tile their L_4 /
+L_6 rows too); sva_wta_hv_d recomputes the checkpointed directions per tile
+and picks d* (sub-pixel within 1e-5 px, observed 0).  The volume / plane
+layout is read from sva_tile_layout_of, so the same checks cover the product
+build (diag_volumes 4) and the §4.11 experiment build (2).
 Ragged widths and heights around the 16 x seg tile, every native D, five
 penalty pairs.  Every entry refuses an undersized buffer with
 SVA_ERR_INVALID_ARG before launching.
@@ -27,9 +30,10 @@ def run_tiles(ctx, sva, torch_dev, C, p):
     H, W, D = C.shape
     lay = sva.tile_layout(W, H, D)
     d_C = dev(C, torch_dev)
-    diag = torch.full((4, H, W, D), 0xAB, dtype=torch.uint8, device=torch_dev)
+    nvol = lay.diag_volumes
+    diag = torch.full((nvol, H, W, D), 0xAB, dtype=torch.uint8, device=torch_dev)
     hck = torch.full((2, H, lay.nsx, D), 0xCD, dtype=torch.uint8, device=torch_dev)
-    vck = torch.full((2, lay.nsy, W, D), 0xEF, dtype=torch.uint8, device=torch_dev)
+    vck = torch.full((6 - nvol, lay.nsy, W, D), 0xEF, dtype=torch.uint8, device=torch_dev)
     assert diag.numel() == lay.diag_bytes and hck.numel() == lay.hckpt_bytes
     assert vck.numel() == lay.vckpt_bytes and d_C.numel() == lay.cost_bytes
     ctx.paths_tile_d(d_C.data_ptr(), d_C.numel(), W, H, p, diag.data_ptr(), diag.numel(),
@@ -54,8 +58,11 @@ def check_stages(oracle, C, dmin, res, P1=10, P2=120):
     diag, hck, vck, disp, sub, lay = res
     seg = lay.seg
     vols = [oracle.path(C, r, P1, P2) for r in range(8)]
-    for r in range(4, 8):
-        assert np.array_equal(diag[r - 4], vols[r]), f"direction {r}"
+    # volumes: the up diagonals 5, 7 (their down pair is recomputed per tile,
+    # DESIGN.md §4.11), or all four diagonals in a build that writes them
+    vol_dirs = [5, 7] if lay.diag_volumes == 2 else [4, 5, 6, 7]
+    for slot, r in enumerate(vol_dirs):
+        assert np.array_equal(diag[slot], vols[r]), f"direction {r}"
     for s in range(lay.nsx):
         if s * seg + seg < W:          # L_0 at the segment's last column
             assert np.array_equal(hck[0, :, s], vols[0][:, s * seg + seg - 1]), ("h0", s)
@@ -66,6 +73,9 @@ def check_stages(oracle, C, dmin, res, P1=10, P2=120):
             assert np.array_equal(vck[0, s], vols[2][s * seg + seg - 1]), ("v0", s)
         if s > 0:                      # L_3 at the segment's first row
             assert np.array_equal(vck[1, s], vols[3][s * seg]), ("v1", s)
+        if lay.diag_volumes == 2 and s * seg + seg < H:   # L_4, L_6 at the last row
+            assert np.array_equal(vck[2, s], vols[4][s * seg + seg - 1]), ("d4", s)
+            assert np.array_equal(vck[3, s], vols[6][s * seg + seg - 1]), ("d6", s)
     S = np.zeros(C.shape, np.uint16)
     for v in vols:
         S += v

@@ -155,7 +155,7 @@ def main():
                 else:
                     wta_hv_call(lib, h)
                 torch.cuda.synchronize()
-                t = L8[:4] if a.entry == "tile" else disp
+                t = L8[:lay.diag_volumes] if a.entry == "tile" else disp
                 outs.append(torch.sum(t.view(torch.int64) if t.dtype == torch.uint8 else
                                       t.to(torch.int64)).item())
                 if a.entry == "tile":
