@@ -145,6 +145,12 @@ constexpr int kCensusCostPx = 128;
 constexpr int kCensusCostPxWide = 128;
 constexpr int kCensusCostRows = 4;
 // Cost-volume stores of census_cost: 1 non-temporal, 0 default policy.
+// Round 4, every width (profiles/r04_v3/ab_store_policy_all.log.txt, frame
+// ms nt / default): default stores speed census_cost up (4K D=256 0.622 ->
+// 0.571 ms) but leave dirty lines whose write-back lands in sgm_paths (4.887
+// -> 4.946), so the frame is equal at 4K D=256 (7.603 / 7.594) and slower
+// elsewhere: 1080p D=128 0.902 / 0.920, D=192 1.332 / 1.342, D=256 1.736 /
+// 1.743, 4K D=128 3.775 / 3.793, 4K D=192 6.042 / 6.078.
 constexpr int kCostStoreNT = 1;
 
 // ---- refpath.hip, Mode R plane kernel v3 ------------------
