@@ -323,7 +323,7 @@ def committed_traffic(workload):
 
 # rocprofv3 kernel names -> bench timer names (the PMC pass reports per kernel)
 PMC_KERNELS = {"sgm_paths_kernel": "sgm_paths", "wta_hv_kernel": "wta_hv",
-               "census_cost_kernel": "cost", "ref_plane3_kernel": "ref_match"}
+               "census_cost_mma_kernel": "cost", "ref_plane3_kernel": "ref_match"}
 MI355X_ENGINE_GHZ = 2.4   # peak engine clock (MI355X_MICROARCH.md)
 SIMDS = 1024              # 256 CUs x 4 SIMDs
 

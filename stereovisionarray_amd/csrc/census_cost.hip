@@ -4,19 +4,23 @@
 // Produces exactly the bytes of census9x7_rows_kernel followed by
 // hamming_cost_rows_kernel -- C[(y*W + x)*D + d] = popcount(CL(x,y) ^
 // CR(x + dir*(dmin+d), y)), 62 where the matched column leaves the image --
-// without the census maps ever reaching HBM, and without the census launch.
+// without the census maps ever reaching HBM, and with the Hamming distances
+// on the matrix cores (round 4; the round-1 kernel computed them with two
+// v_xor + two v_bcnt + a pack per disparity on the VALU).
 //
 // A 256-thread workgroup owns PXB = 128 consecutive pixels of a band of 4
-// rows.  Per row it needs the census words of its own 128 left pixels and of
-// the NW = PXB + D - 1 right-image columns they match against; it forms them
-// from an 8-row LDS ring of image bytes (the 7-row window plus the row being
-// staged), exactly as the census kernel does (aligned dwords realigned with
-// v_alignbyte, one v_sub_sdwa + v_alignbit per bit).  The right census is
-// formed (PXB + D - 1) / PXB ~ 2x over at D = 128 -- VALU the bandwidth-bound
-// cost kernel has spare.  One barrier per row, phase p:
-//   census of row y0+p         -> words[p & 1]          (ring rows y0+p-3..+3)
-//   cost of row y0+p-1         <- words[(p-1) & 1]      (16-byte nt stores)
-//   stage image row y0+p+4     -> ring slot of row y0+p-4 (read by no one now)
+// rows, from an 8-row LDS ring of image bytes (the 7-row window plus the row
+// being staged).  Per row, between two barriers:
+//   A  every census window of the row -- its 128 left pixels and the
+//      PXB + D - 1 right columns they match -- becomes one 64-byte operand
+//      row in LDS, straight from the image bytes (census_bytes: four
+//      comparisons per SWAR step, no census word in between); the staged
+//      costs of the previous row leave as whole 128-byte lines (nt stores);
+//   B  each wave takes one residue class of pixels mod 4 and multiplies its
+//      16-pixel tiles by the right columns' tiles on v_mfma_i32_16x16x64_i8;
+//      each lane packs its four results -- four consecutive disparities of
+//      one pixel -- into a u8x4 word of the staged row; the next image row
+//      is staged into the ring slot nobody reads now.
 // HBM bytes: 1 B/disparity written + ~1.4 B/pixel of image read.
 // dreal < D (a padded frame): disparities d >= dreal get 255.
 #include "sva_device.h"
@@ -27,11 +31,8 @@ namespace sva {
 namespace {
 
 constexpr int CC_BLOCK = 256;
-// pixels per workgroup row, per disparity width (tune::kCensusCostPx*)
-template <int NC> constexpr int pxb_of() { return NC > 8 ? tune::kCensusCostPxWide : tune::kCensusCostPx; }
 constexpr int RING = 8;              // image rows in LDS (power of two)
 constexpr int HX = 4, HY = 3;        // half window (9 wide, 7 high)
-constexpr uint64_t kOutsideCC = 1ull << 63;   // never set in a census word (bits 0..61)
 
 __device__ __forceinline__ void store16_nt(uint8_t* p, const unsigned (&o)[4]) {
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -41,41 +42,113 @@ __device__ __forceinline__ void store16_nt(uint8_t* p, const unsigned (&o)[4]) {
         *(v4u*)p = (v4u){o[0], o[1], o[2], o[3]};
 }
 
-// Census word of the pixel whose 9-byte window row starts at byte s of each
-// ring row; `rows[dy+3]` are the dword views of ring rows y-3 .. y+3.
-__device__ __forceinline__ uint64_t census_at(const unsigned* const* rows, int s) {
-    return census9x7(rows, s >> 2, (unsigned)(s & 3));
+// ---- the Hamming costs on the matrix cores --------------------------------
+// popcount(l ^ r) over the 62 census bits is one integer dot product of
+// K = 64 bytes: with the left word as b_k = 1 - 2 l_k (plus b_63 = popcount(l))
+// and the right word as a_k = r_k (plus a_63 = 1),
+//   sum_k a_k b_k = sum r - 2 sum l r + sum l = popcount(l ^ r).
+// A right column outside the image takes a_k = 1 for every bit and a_63 = 2:
+// 62 - 2 popcount(l) + 2 popcount(l) = 62, the reference's border cost.  The
+// bit order inside K is free (a sum), as long as both operands share it.
+//
+// v_mfma_i32_16x16x64_i8 multiplies 16 right columns (rows M) by 16 left
+// pixels (columns N).  The 16 pixels of an N-tile are one residue class mod 4
+// (stride 4), so every lane's four output rows -- consecutive right columns
+// of one pixel -- are four consecutive disparities starting at a multiple of
+// 4: one u8x4 word of the cost volume, packed with three v_lshl_or.  Tile
+// rows R = 16t + r map to right columns so that d = R - 4n for lane n in
+// either matching direction (DIR < 0 numbers the class's pixels backwards);
+// T = ceil((D + 60) / 16) tiles cover every pixel's D disparities.
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// The 64 operand bytes of one census window straight from the image bytes
+// (no census word in between), 4 comparisons per SWAR step.  rows[0..6] are
+// dword views of ring rows y-3 .. y+3 and the 9-byte window row starts at
+// byte s.  K layout: dwords 2r, 2r+1 = window row r's bytes 0-3, 4-7; dword 14
+// = byte 8 of rows 0-3, dword 15 = byte 8 of rows 4-6 and the bias.  The
+// centre compares with itself (0 in every word), so K holds the 62 census
+// bits plus one position that is 0 on both sides.
+//   PM false (right column, A): byte k = (n_k < c), bias 1;
+//   PM true  (left pixel, B):  byte k = 1 - 2 (n_k < c), bias = popcount.
+template <bool PM>
+__device__ __forceinline__ void census_bytes(const unsigned* const* rows, int s, unsigned (&d)[16]) {
+    const int base = s >> 2;
+    const unsigned sh = (unsigned)(s & 3);
+    unsigned a8[7];
+#pragma unroll
+    for (int r = 0; r < 7; r++) {
+        const unsigned* row = rows[r];
+        const unsigned w0 = row[base], w1 = row[base + 1], w2 = row[base + 2];
+        d[2 * r] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        d[2 * r + 1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        a8[r] = __builtin_amdgcn_alignbyte(w2, w2, sh);     // byte 0 = window byte 8
+    }
+    const unsigned c4 = __builtin_amdgcn_perm(0u, d[7], 0u);  // the centre in all 4 bytes
+    d[14] = __builtin_amdgcn_perm(a8[1], a8[0], 0x0c0c0400u) | __builtin_amdgcn_perm(a8[3], a8[2], 0x04000c0cu);
+    d[15] = __builtin_amdgcn_perm(a8[5], a8[4], 0x0c0c0400u) | ((a8[6] & 0xffu) << 16);
+    // per byte x < c: where the top bits differ, c's top bit; else the low 7
+    // bits' borrow, (c7 | 0x80) - 1 - x7 (no byte borrows into the next)
+    const unsigned cH1 = (c4 | 0x80808080u) - 0x01010101u;
+    unsigned sum = 0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const unsigned x = d[q];
+        const unsigned t3 = cH1 - (x & 0x7f7f7f7fu);
+        const unsigned m = x ^ c4;
+        const unsigned lt = (m & c4) | (~m & t3);            // v_bfi_b32: top bit = x < c
+        const unsigned b01 = (lt >> 7) & 0x01010101u;
+        if constexpr (PM) {
+            sum += q < 15 ? b01 : (b01 & 0x00ffffffu);     // bytes <= 16: no carry
+            d[q] = __builtin_amdgcn_perm(0x0000ff01u, 0u, b01 | 0x04040404u);
+        } else {
+            d[q] = b01;
+        }
+    }
+    if constexpr (PM) {
+        const unsigned pc = __builtin_amdgcn_sad_u8(sum, 0u, 0u);   // byte sum
+        d[15] = (d[15] & 0x00ffffffu) | (pc << 24);
+    } else {
+        d[15] = (d[15] & 0x00ffffffu) | 0x01000000u;
+    }
 }
 
-template <int NC>
-__global__ __launch_bounds__(CC_BLOCK) void census_cost_kernel(
+template <int NC, int DIR>
+__global__ __launch_bounds__(CC_BLOCK) void census_cost_mma_kernel(
     const uint8_t* __restrict__ left, const uint8_t* __restrict__ right, int W, int H,
-    size_t pitch, int dmin, int dir, int rows, int dreal, uint8_t* __restrict__ C) {
+    size_t pitch, int dmin, int rows, int dreal, uint8_t* __restrict__ C) {
     constexpr int D = NC * 16;
-    constexpr int PXB = pxb_of<NC>();
-    constexpr int NW = PXB + D - 1;                      // right census words per row
-    constexpr int RW = (NW + 8 + 4 + 3) / 4 * 4;         // right ring row bytes (+ dword overrun)
+    constexpr int PXB = 128;                             // pixels per workgroup row
+    constexpr int NSPAN = PXB / 64;                      // N-tiles per residue class
+    constexpr int T = (D + 60 + 15) / 16;                // M-tiles per N-tile (16 T = D + 64)
+    constexpr int NWM = PXB + D - 1;                     // right columns some pixel matches
+    // operand rows: 16 front rows + NWM, rounded to 16 (planes 256-B aligned); the
+    // tiles' last 4 rows (d >= D for every pixel) read the padding rows
+    constexpr int NWMP = (16 + NWM + 4 + 15) / 16 * 16;
+    constexpr int RW = (NWM + 8 + 4 + 3) / 4 * 4;        // right ring row bytes (+ dword overrun)
     constexpr int LW = (PXB + 8 + 4 + 3) / 4 * 4;        // left ring row bytes
-    constexpr int SPAN = NW + 8 + PXB + 8;               // image bytes staged per row
+    constexpr int SPAN = NWM + 8 + PXB + 8;              // image bytes staged per row
     constexpr int LOADS = (SPAN + CC_BLOCK - 1) / CC_BLOCK;
-    constexpr int NWORDS = NW + PXB;                     // census words formed per row
+    constexpr int NWORDS = PXB + NWM;                    // census words formed per row (left first)
     constexpr int WPT = (NWORDS + CC_BLOCK - 1) / CC_BLOCK;
-    static_assert(PXB % 64 == 0 && NC % 4 == 0, "cost tasks must tile the workgroup");
+    // staging dwords per pixel slot: the D / 4 words, then 4 dump words (lane
+    // quarter q's word when it holds no disparity of this pixel) and 3 spare;
+    // S4 = 3 mod 4 keeps a wave's 32-lane write groups on distinct banks
+    constexpr int S4 = NC * 4 + 7;
+    static_assert(CC_BLOCK == 256 && PXB % 64 == 0, "four waves, one residue class each");
     __shared__ __attribute__((aligned(16))) uint8_t ringR[RING][RW];
     __shared__ __attribute__((aligned(16))) uint8_t ringL[RING][LW];
-    __shared__ uint64_t rw[2][NW];
-    __shared__ uint64_t lw[2][PXB];
+    __shared__ __attribute__((aligned(16))) uint8_t opA[4 * NWMP * 16];   // [K quarter][column][16]
+    __shared__ __attribute__((aligned(16))) uint8_t opB[4 * PXB * 16];    // [K quarter][pixel][16]
+    __shared__ unsigned stg[PXB * S4];                                     // [pixel slot][S4]
 
     const int bpr = (W + PXB - 1) / PXB;
     const int bx = blockIdx.x % bpr, by = blockIdx.x / bpr;
     const int x0 = bx * PXB, y0 = by * rows;
     const int nrows = min(H, y0 + rows) - y0;
     const int t = threadIdx.x;
-    // right word j <-> column colR(j); ring byte i <-> image column cbR + i
-    const int colR0 = dir > 0 ? x0 + dmin : x0 + PXB - 1 - dmin;        // column of word 0
-    const int cminR = dir > 0 ? colR0 : colR0 - (NW - 1);
-    const int cbR = cminR - HX, cbL = x0 - HX;
-    const bool border = cminR < 0 || cminR + NW > W;
+    // operand row 16 + i of opA <-> right column xlo + i; ring byte i <-> column cbR + i
+    const int xlo = DIR > 0 ? x0 + dmin : x0 + 1 - dmin - D;
+    const int cbR = xlo - HX, cbL = x0 - HX;
 
     auto fetch = [&](int gy, uint8_t (&v)[LOADS]) {
 #pragma unroll
@@ -83,8 +156,8 @@ __global__ __launch_bounds__(CC_BLOCK) void census_cost_kernel(
             const int i = t + k * CC_BLOCK;
             int col;
             const uint8_t* img;
-            if (i < NW + 8) { col = cbR + i; img = right; }
-            else { col = cbL + (i - (NW + 8)); img = left; }
+            if (i < NWM + 8) { col = cbR + i; img = right; }
+            else { col = cbL + (i - (NWM + 8)); img = left; }
             v[k] = (i < SPAN && (unsigned)col < (unsigned)W && (unsigned)gy < (unsigned)H)
                        ? img[(size_t)gy * pitch + col] : 0;
         }
@@ -94,13 +167,18 @@ __global__ __launch_bounds__(CC_BLOCK) void census_cost_kernel(
 #pragma unroll
         for (int k = 0; k < LOADS; k++) {
             const int i = t + k * CC_BLOCK;
-            if (i < NW + 8) ringR[slot][i] = v[k];
-            else if (i < SPAN) ringL[slot][i - (NW + 8)] = v[k];
+            if (i < NWM + 8) ringR[slot][i] = v[k];
+            else if (i < SPAN) ringL[slot][i - (NWM + 8)] = v[k];
         }
     };
+    auto put_row = [&](uint8_t* op, int nrow, int row, const unsigned (&d)[16]) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int q4 = 0; q4 < 4; q4++)
+            *reinterpret_cast<v4u*>(&op[(q4 * nrow + row) * 16]) =
+                (v4u){d[4 * q4], d[4 * q4 + 1], d[4 * q4 + 2], d[4 * q4 + 3]};
+    };
 
-    // prologue: rows y0-3 .. y0+3 in the ring, row y0+4 in registers
-    // (all 8 rows' loads are issued before any is waited on)
     uint8_t pro[2 * HY + 1][LOADS];
 #pragma unroll
     for (int r = -HY; r <= HY; r++) fetch(y0 + r, pro[r + HY]);
@@ -110,8 +188,10 @@ __global__ __launch_bounds__(CC_BLOCK) void census_cost_kernel(
     for (int r = -HY; r <= HY; r++) stage(y0 + r, pro[r + HY]);
     __syncthreads();
 
+    const int wv = t >> 6, l = t & 63, ln = l & 15, lq = l >> 4;
     for (int p = 0; p <= nrows; p++) {
-        if (p < nrows) {                                  // census of row y
+        // ---- census of row y0+p into the operand rows; store of row y0+p-1
+        if (p < nrows) {
             const int y = y0 + p;
             const bool yin = y >= HY && y < H - HY;
             const unsigned* rR[7];
@@ -121,79 +201,96 @@ __global__ __launch_bounds__(CC_BLOCK) void census_cost_kernel(
                 rR[dy + HY] = reinterpret_cast<const unsigned*>(ringR[(y + dy) & (RING - 1)]);
                 rL[dy + HY] = reinterpret_cast<const unsigned*>(ringL[(y + dy) & (RING - 1)]);
             }
-            uint64_t* rwb = rw[p & 1];
-            uint64_t* lwb = lw[p & 1];
 #pragma unroll
             for (int k = 0; k < WPT; k++) {
                 const int w = t + k * CC_BLOCK;
-                if (w < NW) {
-                    const int col = dir > 0 ? colR0 + w : colR0 - w;
-                    uint64_t word;
-                    if ((unsigned)col >= (unsigned)W) word = kOutsideCC;
-                    else if (!yin || col < HX || col >= W - HX) word = 0;
-                    else word = census_at(rR, col - cminR);
-                    rwb[w] = word;
+                unsigned d[16];
+                if (w < PXB) {
+                    // operand row b <-> pixel 4 (b % (PXB/4)) + b / (PXB/4): the
+                    // rows of one residue class are consecutive
+                    const int b = w;
+                    const int lp = 4 * (b % (PXB / 4)) + b / (PXB / 4), x = x0 + lp;
+                    if (yin && x >= HX && x < W - HX) {
+                        census_bytes<true>(rL, lp, d);
+                    } else {                                       // census word 0
+#pragma unroll
+                        for (int q = 0; q < 15; q++) d[q] = 0x01010101u;
+                        d[15] = 0x00010101u;                       // b_63 = popcount 0
+                    }
+                    put_row(opB, PXB, b, d);
                 } else if (w < NWORDS) {
-                    const int lp = w - NW, x = x0 + lp;
-                    uint64_t word = 0;
-                    if (yin && x >= HX && x < W - HX) word = census_at(rL, lp);
-                    lwb[lp] = word;
+                    const int i = w - PXB, col = xlo + i;
+                    if ((unsigned)col >= (unsigned)W) {
+                        // outside: a_k = 1 on the 62 census positions (not the
+                        // centre, dword 7 byte 0), a_63 = 2 -> cost 62
+#pragma unroll
+                        for (int q = 0; q < 15; q++) d[q] = 0x01010101u;
+                        d[7] = 0x01010100u;
+                        d[15] = 0x02010101u;
+                    } else if (yin && col >= HX && col < W - HX) {
+                        census_bytes<false>(rR, i, d);
+                    } else {                                       // census word 0
+#pragma unroll
+                        for (int q = 0; q < 15; q++) d[q] = 0u;
+                        d[15] = 0x01000000u;                       // a_63 = 1
+                    }
+                    put_row(opA, NWMP, 16 + i, d);
                 }
             }
         }
-        if (p > 0) {                                      // cost of row y - 1
+        if (p > 0) {
+            // pixel lp's slot: class c = lp & 3, span s = lp >> 6, lane n
             const int y = y0 + p - 1;
-            const uint64_t* rwb = rw[(p - 1) & 1];
-            const uint64_t* lwb = lw[(p - 1) & 1];
-            // a wave owns 16 pixels x all NC chunks per pass (lane (p, c) forms
-            // chunks c, c+4, ...), so each 128-byte line is written by one wave
-            // in back-to-back instructions; each 32-lane LDS group reads 16
-            // pixels x 2 chunks: 32 consecutive words, conflict-free
-            const int wv = t >> 6, ln = t & 63;
-            const int pl = ln & 15, c0 = ln >> 4;
 #pragma unroll
-            for (int k = 0; k < PXB / 64; k++) {
-                const int lp = 16 * (wv + 4 * k) + pl;
-                const int x = x0 + lp;
+            for (int k = 0; k < PXB * NC / CC_BLOCK; k++) {
+                const int ch = t + k * CC_BLOCK;
+                const int lp = ch / NC, ci = ch % NC, x = x0 + lp;
                 if (x >= W) continue;
-                const uint64_t lc = lwb[lp];
-                const uint64_t* base = rwb + (dir > 0 ? lp : PXB - 1 - lp);
+                const int m = (lp >> 2) & 15, n = DIR > 0 ? m : 15 - m;
+                const unsigned* src = &stg[((lp & 3) * (PXB / 4) + 16 * (lp >> 6) + n) * S4 + 4 * ci];
+                unsigned out[4] = {src[0], src[1], src[2], src[3]};
+                if (dreal < D) {                 // padded disparities: cost 255
 #pragma unroll
-                for (int cc = 0; cc < NC / 4; cc++) {
-                    const int c = c0 + 4 * cc;
-                    const uint64_t* src = base + 16 * c;
-                    unsigned out[4];
-                    if (!border) {
-#pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            unsigned ww = 0;
-#pragma unroll
-                            for (int b = 0; b < 4; b++)
-                                ww |= (unsigned)__popcll(lc ^ src[q * 4 + b]) << (8 * b);
-                            out[q] = ww;
-                        }
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            unsigned ww = 0;
-#pragma unroll
-                            for (int b = 0; b < 4; b++) {
-                                const uint64_t v = lc ^ src[q * 4 + b];
-                                const unsigned cst = (v >> 63) ? 62u : (unsigned)__popcll(v);
-                                ww |= cst << (8 * b);
-                            }
-                            out[q] = ww;
-                        }
-                    }
-                    if (dreal < D) {                 // padded disparities: cost 255
-#pragma unroll
-                        for (int q = 0; q < 4; q++) out[q] |= pad_bytes(16 * c + 4 * q, dreal);
-                    }
-                    store16_nt(C + ((size_t)y * W + x) * D + 16 * c, out);
+                    for (int q = 0; q < 4; q++) out[q] |= pad_bytes(16 * ci + 4 * q, dreal);
                 }
+                store16_nt(C + ((size_t)y * W + x) * D + 16 * ci, out);
             }
         }
-        if (p < nrows) {                                  // stage row y0+p+4, fetch the next
+        __syncthreads();
+        // ---- the costs of row y0+p on the matrix cores, into the staging rows
+        if (p < nrows) {
+            const int c = wv;                                   // this wave's residue class
+            const v4i zero = {0, 0, 0, 0};
+#pragma unroll
+            for (int s = 0; s < NSPAN; s++) {
+                const int m = DIR > 0 ? ln : 15 - ln;
+                const v4i bf = *reinterpret_cast<const v4i*>(
+                    &opB[(lq * PXB + c * (PXB / 4) + 16 * s + m) * 16]);
+                // lane (n = ln, q = lq) holds rows 16 tt + 4q + i = disparities 4j + i;
+                // tiles go in groups of G (G fragments + G accumulators live)
+                unsigned* dst = &stg[(c * (PXB / 4) + 16 * s + ln) * S4];
+                constexpr int G = 4;
+#pragma unroll
+                for (int g = 0; g < T; g += G) {
+                    v4i acc[G];
+#pragma unroll
+                    for (int i = 0; i < G && g + i < T; i++) {
+                        // row R = 4 n + d of pixel lane n (DIR < 0: that class's pixel 15 - n)
+                        const int R = 16 * (g + i) + ln;
+                        const int idx = DIR > 0 ? 64 * s + c + R : 64 * s + c + D + 59 - R;
+                        const v4i af = *reinterpret_cast<const v4i*>(&opA[(lq * NWMP + 16 + idx) * 16]);
+                        acc[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf, zero, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int i = 0; i < G && g + i < T; i++) {
+                        const int j = 4 * (g + i) + lq - ln;
+                        unsigned wd = (unsigned)acc[i][0] | ((unsigned)acc[i][1] << 8);
+                        wd |= ((unsigned)acc[i][2] << 16) | ((unsigned)acc[i][3] << 24);
+                        dst[(unsigned)j < (unsigned)(NC * 4) ? j : NC * 4 + lq] = wd;   // else: dump
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
             stage(y0 + p + HY + 1, pre);
             if (p + 1 < nrows) fetch(y0 + p + HY + 2, pre);
         }
@@ -210,17 +307,22 @@ hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right,
     if (dreal <= 0) dreal = D;
     ScopedKernelTimer t(c, "cost");
     const int rows = tune::kCensusCostRows;
-    const int PXB = D > 128 ? pxb_of<16>() : pxb_of<8>();
-    const int bpr = (W + PXB - 1) / PXB;
-    const dim3 grid((unsigned)(bpr * ((H + rows - 1) / rows)));
-    const int sd = dir > 0 ? 1 : -1;
+    const dim3 grid((unsigned)(((W + 127) / 128) * ((H + rows - 1) / rows)));   // 128 px x rows
+#define SVA_CC_MMA(NC_)                                                                            \
+    if (dir > 0)                                                                                   \
+        hipLaunchKernelGGL((census_cost_mma_kernel<NC_, 1>), grid, dim3(CC_BLOCK), 0, c.stream, left, \
+                           right, W, H, pitch, dmin, rows, dreal, C);                             \
+    else                                                                                           \
+        hipLaunchKernelGGL((census_cost_mma_kernel<NC_, -1>), grid, dim3(CC_BLOCK), 0, c.stream,     \
+                           left, right, W, H, pitch, dmin, rows, dreal, C);
     switch (D) {
-        case 64: hipLaunchKernelGGL(census_cost_kernel<4>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
-        case 128: hipLaunchKernelGGL(census_cost_kernel<8>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
-        case 192: hipLaunchKernelGGL(census_cost_kernel<12>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
-        case 256: hipLaunchKernelGGL(census_cost_kernel<16>, grid, dim3(CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin, sd, rows, dreal, C); break;
+        case 64: SVA_CC_MMA(4) break;
+        case 128: SVA_CC_MMA(8) break;
+        case 192: SVA_CC_MMA(12) break;
+        case 256: SVA_CC_MMA(16) break;
         default: return hipErrorInvalidValue;
     }
+#undef SVA_CC_MMA
     return hipGetLastError();
 }
 

@@ -239,11 +239,9 @@ int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int
         SVA_HIP(c, c->disp_r.ensure(np * 2), "lr workspace");
         dr = (uint16_t*)c->disp_r.ptr;
     }
-    if (p->dir_y == 0 && Dp >= 128 && census_cost_supported(Dp)) {
+    if (p->dir_y == 0 && Dp >= tune::kCensusCostMinD && census_cost_supported(Dp)) {
         // census maps stay on chip: one census+cost kernel (census_cost.hip),
-        // once per matching role when the L/R check runs.
-        // In-process A/B per frame at 1080p: D=128 1.129 -> 1.112 ms,
-        // D=192 1.646 -> 1.588 ms; D=64 is faster split (0.609 vs 0.650 ms).
+        // once per matching role when the L/R check runs (DESIGN §4.2).
         SVA_HIP(c, launch_census_cost(*c, left, right, W, H, pitch, Dp, p->dmin, p->dir, C, p->D),
                 "cost launch");
         if ((s = paths_wta(c, C, W, H, p, Dp, disp, sub))) return s;
@@ -323,7 +321,7 @@ int run_sgm_batch(Ctx* c, const sva_pair_d* jobs, int n, int W, int H, size_t pi
         uint8_t* Ci = C + (size_t)i * nv;
         if (ns > 1) c->stream = c->side[i % ns];
         hipError_t e;
-        if (q->dir_y == 0 && Dp >= 128 && census_cost_supported(Dp)) {
+        if (q->dir_y == 0 && Dp >= tune::kCensusCostMinD && census_cost_supported(Dp)) {
             e = launch_census_cost(*c, jobs[i].left, jobs[i].right, W, H, pitch, Dp, q->dmin, q->dir,
                                    Ci, q->D);
         } else {

@@ -133,24 +133,26 @@ constexpr size_t kBatchMaxBytes = (size_t)24 << 30;
 // ---- census.hip / census_cost.hip / cost.hip ------------
 // Rows per workgroup of the multi-row census kernel.
 constexpr int kCensusRows = 16;
-// census_cost: pixels per workgroup row and rows per workgroup; 128 px x 4
-// rows was the best of 64/128/256 px x 2/4/8/16 rows (0.093 ms at 1080p
-// D=128, profiles/r01_v8/ab_census_cost_tiling.jsonl); 192 / 256 px measured
-// 0.093 / 0.101 ms in round 2.
-constexpr int kCensusCostPx = 128;
-// D > 128 on its own constant: 192 / 256 px form 25-37 % fewer census words
-// there, yet census_cost ran slower in round 3 (1080p D=256 0.149 -> 0.184 /
-// 0.193 ms, D=192 0.123 -> 0.139 / 0.145 ms, 4K D=256 0.705 -> 0.713 / 0.732
-// ms; profiles/r03_v8/ab_census_cost_wide_tiles.log.txt).
-constexpr int kCensusCostPxWide = 128;
+// Frames of D >= this (1-D steps) run census_cost; smaller D run the census
+// kernel + the cost kernel.  The round-1 VALU kernel lost at D=64 (0.609 vs
+// 0.650 ms at 1080p, so 128 until round 4); the MFMA kernel wins there too,
+// frame ms split / census_cost (profiles/r04_v3/ab_d64_route.log.txt): 1080p
+// 0.5247 / 0.5224, 640x480 0.1499 / 0.1422, 960x540 0.1862 / 0.1824.
+constexpr int kCensusCostMinD = 64;
+// census_cost: rows per workgroup (128 px x 4 rows was the best of 64/128/256
+// px x 2/4/8/16 rows for the round-1 VALU kernel,
+// profiles/r01_v8/ab_census_cost_tiling.jsonl; the MFMA kernel keeps it).
 constexpr int kCensusCostRows = 4;
 // Cost-volume stores of census_cost: 1 non-temporal, 0 default policy.
-// Round 4, every width (profiles/r04_v3/ab_store_policy_all.log.txt, frame
-// ms nt / default): default stores speed census_cost up (4K D=256 0.622 ->
-// 0.571 ms) but leave dirty lines whose write-back lands in sgm_paths (4.887
-// -> 4.946), so the frame is equal at 4K D=256 (7.603 / 7.594) and slower
-// elsewhere: 1080p D=128 0.902 / 0.920, D=192 1.332 / 1.342, D=256 1.736 /
-// 1.743, 4K D=128 3.775 / 3.793, 4K D=192 6.042 / 6.078.
+// Round 4, every width, on the VALU kernel
+// (profiles/r04_v3/ab_store_policy_all.log.txt, frame ms nt / default):
+// default stores speed census_cost up (4K D=256 0.622 -> 0.571 ms) but leave
+// dirty lines whose write-back lands in sgm_paths (4.887 -> 4.946), so the
+// frame is equal at 4K D=256 (7.603 / 7.594) and slower elsewhere: 1080p
+// D=128 0.902 / 0.920, D=192 1.332 / 1.342, D=256 1.736 / 1.743, 4K D=128
+// 3.775 / 3.793, 4K D=192 6.042 / 6.078.  The MFMA kernel stages each row
+// and stores whole 128-byte lines, nt (single 4-byte nt stores from the MFMA
+// lanes: census_cost 0.57 ms at 1080p D=128, ab_census_cost_mfma.log.txt).
 constexpr int kCostStoreNT = 1;
 
 // ---- refpath.hip, Mode R plane kernel v3 ------------------

@@ -22,7 +22,7 @@ SHORT = {
     "sgm_paths_kernel": "sgm_paths",
     "hamming_cost2_kernel": "cost2", "fuse_depth_kernel": "fuse_depth",
     "hamming_cost_rows_kernel": "cost", "census9x7_rows_kernel": "census",
-    "census_cost_kernel": "cost", "wta_h_kernel": "wta_h",
+    "census_cost_mma_kernel": "cost", "wta_hv_kernel": "wta_hv",
 }
 
 
