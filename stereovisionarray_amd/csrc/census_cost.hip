@@ -112,12 +112,18 @@ __device__ __forceinline__ void census_bytes(const unsigned* const* rows, int s,
     }
 }
 
+// pixels per workgroup row (a multiple of 64: 4 residue classes x 16)
+template <int NC> constexpr int mma_px() {
+    return NC == 4 ? tune::kCensusCostPx4 : NC == 8 ? tune::kCensusCostPx8
+                   : NC == 12 ? tune::kCensusCostPx12 : tune::kCensusCostPx16;
+}
+
 template <int NC, int DIR>
 __global__ __launch_bounds__(CC_BLOCK) void census_cost_mma_kernel(
     const uint8_t* __restrict__ left, const uint8_t* __restrict__ right, int W, int H,
     size_t pitch, int dmin, int rows, int dreal, uint8_t* __restrict__ C) {
     constexpr int D = NC * 16;
-    constexpr int PXB = 128;                             // pixels per workgroup row
+    constexpr int PXB = mma_px<NC>();                    // pixels per workgroup row
     constexpr int NSPAN = PXB / 64;                      // N-tiles per residue class
     constexpr int T = (D + 60 + 15) / 16;                // M-tiles per N-tile (16 T = D + 64)
     constexpr int NWM = PXB + D - 1;                     // right columns some pixel matches
@@ -307,7 +313,8 @@ hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right,
     if (dreal <= 0) dreal = D;
     ScopedKernelTimer t(c, "cost");
     const int rows = tune::kCensusCostRows;
-    const dim3 grid((unsigned)(((W + 127) / 128) * ((H + rows - 1) / rows)));   // 128 px x rows
+    const int px = D == 64 ? mma_px<4>() : D == 128 ? mma_px<8>() : D == 192 ? mma_px<12>() : mma_px<16>();
+    const dim3 grid((unsigned)(((W + px - 1) / px) * ((H + rows - 1) / rows)));
 #define SVA_CC_MMA(NC_)                                                                            \
     if (dir > 0)                                                                                   \
         hipLaunchKernelGGL((census_cost_mma_kernel<NC_, 1>), grid, dim3(CC_BLOCK), 0, c.stream, left, \

@@ -143,6 +143,13 @@ constexpr int kCensusCostMinD = 64;
 // px x 2/4/8/16 rows for the round-1 VALU kernel,
 // profiles/r01_v8/ab_census_cost_tiling.jsonl; the MFMA kernel keeps it).
 constexpr int kCensusCostRows = 4;
+// census_cost_mma_kernel: pixels per workgroup row at D = 64 / 128 / 192 /
+// 256.  64 px hold 5 / 4 / 3 workgroups per CU where 128 px hold 4 / 3 / 2 /
+// 2 (LDS), but form 4 census windows per pixel instead of 3.  census_cost ms
+// 128 / 64 px (profiles/r04_v3/ab_census_cost_px.log.txt): 1080p D=64 0.0673
+// / 0.0669, 640x480 D=64 0.0193 / 0.0159, D=128 0.0975 / 0.0985, D=192 0.1409
+// / 0.1360, D=256 0.1567 / 0.1744, 4K D=256 0.630 / 0.676.
+constexpr int kCensusCostPx4 = 64, kCensusCostPx8 = 128, kCensusCostPx12 = 64, kCensusCostPx16 = 128;
 // Cost-volume stores of census_cost: 1 non-temporal, 0 default policy.
 // Round 4, every width, on the VALU kernel
 // (profiles/r04_v3/ab_store_policy_all.log.txt, frame ms nt / default):
