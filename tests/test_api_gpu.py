@@ -110,8 +110,14 @@ def test_reserve_timing_and_errors(ctx, sva):
         ms, n = ctx.kernel_time(name)
         assert n == 2 and ms > 0.0, name
     assert ctx.kernel_time("wta") == (0.0, 0) and ctx.kernel_time("wta_h") == (0.0, 0)
-    # 1-D steps without the L/R check, D >= 128: census and cost are one kernel ("cost")
+    # 1-D steps without the L/R check: census and cost are one kernel ("cost"),
+    # D = 64 included (tune::kCensusCostMinD, round 4)
     assert ctx.kernel_time("census") == (0.0, 0)
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    ctx.disparity_sgm(L, R, sva.default_params(D=64))
+    ctx.set_timing(False)
+    assert ctx.kernel_time("census") == (0.0, 0) and ctx.kernel_time("cost")[1] == 1
     # AUTO (the default) and COST_VOLUME are the same route, D = 256 included
     L2, R2, _ = synth.stereo_pair(64, 320, 256, 0, -1, seed=3)
     for kern in (sva.SVA_PATH_KERNEL_AUTO, sva.SVA_PATH_KERNEL_COST_VOLUME):

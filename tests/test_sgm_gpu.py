@@ -172,8 +172,8 @@ def test_full_pipeline_device_buffers(ctx, sva, oracle, torch_dev):
     assert np.array_equal(host(disp).view(np.uint16), od)
 
 
-# D = 64 runs census + cost kernels, D >= 128 the census+cost kernel for both
-# matching roles (the right-reference pass swaps the images, not census maps)
+# 1-D steps run the census+cost kernel at every D (D = 64 since round 4) for
+# both matching roles (the right-reference pass swaps the images, not census maps)
 @pytest.mark.parametrize("D,dir,dmin", [(64, -1, 0), (128, -1, 0), (128, 1, 3), (192, -1, 2)])
 def test_lr_check(ctx, sva, oracle, D, dir, dmin):
     W, H = 300, 60
