@@ -47,9 +47,11 @@ __device__ __forceinline__ void store16_nt(uint8_t* p, const unsigned (&o)[4]) {
 // K = 64 bytes: with the left word as b_k = 1 - 2 l_k (plus b_63 = popcount(l))
 // and the right word as a_k = r_k (plus a_63 = 1),
 //   sum_k a_k b_k = sum r - 2 sum l r + sum l = popcount(l ^ r).
-// A right column outside the image takes a_k = 1 for every bit and a_63 = 2:
+// A right column outside the image takes a_k = 1 on its 62 census positions
+// (0 at the window centre's, which is 0 in every left word too) and a_63 = 2:
 // 62 - 2 popcount(l) + 2 popcount(l) = 62, the reference's border cost.  The
-// bit order inside K is free (a sum), as long as both operands share it.
+// bit order inside K is free (a sum), as long as both operands share it
+// (tests/test_mfma_hamming_cpu.py restates all of this against the oracle).
 //
 // v_mfma_i32_16x16x64_i8 multiplies 16 right columns (rows M) by 16 left
 // pixels (columns N).  The 16 pixels of an N-tile are one residue class mod 4
