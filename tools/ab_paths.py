@@ -56,7 +56,10 @@ def main():
         raise SystemExit(f"--entry {a.entry} needs D in 64/128/192/256")
     lay = sva.tile_layout(W, H, D) if native else None
     HCK = torch.zeros(lay.hckpt_bytes, dtype=torch.uint8, device=dev) if native else None
-    VCK = torch.zeros(lay.vckpt_bytes, dtype=torch.uint8, device=dev) if native else None
+    # vertical checkpoints at the largest layout any variant reports: 6 planes
+    # (§4.11 builds that recompute diagonals carry their row checkpoints here)
+    VCK = torch.zeros(lay.vckpt_bytes // (6 - lay.diag_volumes) * 6, dtype=torch.uint8,
+                      device=dev) if native else None
     vp = ct.c_void_p
 
     def tile_call(lib, h):
@@ -97,7 +100,7 @@ def main():
     torch.cuda.synchronize()
     C_ref = C_src.clone()          # census -> cost bytes, checked against every census_cost variant
     # tile-stage volumes and checkpoints for the wta_hv entry (first library)
-    if native:
+    if native and a.entry in ("tile", "wta_hv"):
         assert tile_call(lib0, h0) == 0
     torch.cuda.synchronize()
     times = {n: [] for n, _, _ in handles}
