@@ -8,10 +8,11 @@
 // on the matrix cores (round 4; the round-1 kernel computed them with two
 // v_xor + two v_bcnt + a pack per disparity on the VALU).
 //
-// A 256-thread workgroup owns PXB = 128 consecutive pixels of a band of 4
-// rows, from an 8-row LDS ring of image bytes (the 7-row window plus the row
-// being staged).  Per row, between two barriers:
-//   A  every census window of the row -- its 128 left pixels and the
+// A 256-thread workgroup owns PXB = 64 or 128 consecutive pixels (per D,
+// tune::kCensusCostPx*) of a band of 8 rows (4 for frames too small to fill
+// the chip that way), from an 8-row LDS ring of image bytes (the 7-row window
+// plus the row being staged).  Per row, between two barriers:
+//   A  every census window of the row -- its PXB left pixels and the
 //      PXB + D - 1 right columns they match -- becomes one 64-byte operand
 //      row in LDS, straight from the image bytes (census_bytes: four
 //      comparisons per SWAR step, no census word in between); the staged
@@ -314,9 +315,13 @@ hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right,
                               size_t pitch, int D, int dmin, int dir, uint8_t* C, int dreal) {
     if (dreal <= 0) dreal = D;
     ScopedKernelTimer t(c, "cost");
-    const int rows = tune::kCensusCostRows;
     const int px = D == 64 ? mma_px<4>() : D == 128 ? mma_px<8>() : D == 192 ? mma_px<12>() : mma_px<16>();
-    const dim3 grid((unsigned)(((W + px - 1) / px) * ((H + rows - 1) / rows)));
+    const long long bpr = (W + px - 1) / px;
+    const int rows = bpr * ((H + tune::kCensusCostRows - 1) / tune::kCensusCostRows) >=
+                             tune::kCensusCostMinGroups
+                         ? tune::kCensusCostRows
+                         : tune::kCensusCostRowsSmall;
+    const dim3 grid((unsigned)(bpr * ((H + rows - 1) / rows)));
 #define SVA_CC_MMA(NC_)                                                                            \
     if (dir > 0)                                                                                   \
         hipLaunchKernelGGL((census_cost_mma_kernel<NC_, 1>), grid, dim3(CC_BLOCK), 0, c.stream, left, \

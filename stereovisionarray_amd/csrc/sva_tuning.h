@@ -139,10 +139,17 @@ constexpr int kCensusRows = 16;
 // frame ms split / census_cost (profiles/r04_v3/ab_d64_route.log.txt): 1080p
 // 0.5247 / 0.5224, 640x480 0.1499 / 0.1422, 960x540 0.1862 / 0.1824.
 constexpr int kCensusCostMinD = 64;
-// census_cost: rows per workgroup (128 px x 4 rows was the best of 64/128/256
-// px x 2/4/8/16 rows for the round-1 VALU kernel,
-// profiles/r01_v8/ab_census_cost_tiling.jsonl; the MFMA kernel keeps it).
-constexpr int kCensusCostRows = 4;
+// census_cost: rows per workgroup.  The MFMA kernel prefers 8 (census_cost ms
+// at 2 / 4 / 8 / 16 rows, profiles/r04_v4/ab_census_cost_rows.log.txt: 1080p
+// D=128 0.1063 / 0.0974 / 0.0938 / 0.1062, D=64 0.0789 / 0.0676 / 0.0648 /
+// 0.0674, D=256 0.1763 / 0.1572 / 0.1488 / 0.1501, 4K D=128 0.399 / 0.366 /
+// 0.342 / 0.353) unless that leaves fewer than kCensusCostMinGroups
+// workgroups: 640x480 D=64 (600 workgroups at 8 rows) 0.0173 / 0.0162 /
+// 0.0196 / 0.0275.  (The round-1 VALU kernel had 4 as the best of 2-16,
+// profiles/r01_v8/ab_census_cost_tiling.jsonl.)
+constexpr int kCensusCostRows = 8;
+constexpr int kCensusCostRowsSmall = 4;
+constexpr int kCensusCostMinGroups = 1536;   // 6 per CU
 // census_cost_mma_kernel: pixels per workgroup row at D = 64 / 128 / 192 /
 // 256.  64 px hold 5 / 4 / 3 workgroups per CU where 128 px hold 4 / 3 / 2 /
 // 2 (LDS), but form 4 census windows per pixel instead of 3.  census_cost ms
