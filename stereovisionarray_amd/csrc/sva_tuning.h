@@ -152,11 +152,16 @@ constexpr int kCensusCostRowsSmall = 4;
 constexpr int kCensusCostMinGroups = 1536;   // 6 per CU
 // census_cost_mma_kernel: pixels per workgroup row at D = 64 / 128 / 192 /
 // 256.  64 px hold 5 / 4 / 3 workgroups per CU where 128 px hold 4 / 3 / 2 /
-// 2 (LDS), but form 4 census windows per pixel instead of 3.  census_cost ms
-// 128 / 64 px (profiles/r04_v3/ab_census_cost_px.log.txt): 1080p D=64 0.0673
-// / 0.0669, 640x480 D=64 0.0193 / 0.0159, D=128 0.0975 / 0.0985, D=192 0.1409
-// / 0.1360, D=256 0.1567 / 0.1744, 4K D=256 0.630 / 0.676.
-constexpr int kCensusCostPx4 = 64, kCensusCostPx8 = 128, kCensusCostPx12 = 64, kCensusCostPx16 = 128;
+// 2 (LDS), but form 4 census windows per pixel instead of 3.  At 4 rows per
+// workgroup, census_cost ms 128 / 64 px (profiles/r04_v3/ab_census_cost_px.log.txt):
+// 1080p D=64 0.0673 / 0.0669, 640x480 D=64 0.0193 / 0.0159, D=128 0.0975 /
+// 0.0985, D=192 0.1409 / 0.1360, D=256 0.1567 / 0.1744.  Re-measured at 8
+// rows (profiles/r04_v4/ab_census_cost_px_rows8.log.txt), D=128 turns to 64
+// px: 1080p 0.0954 / 0.0913 (also with dir +1: 0.0954 / 0.0915), 4K 0.343 /
+// 0.333, 960x540 0.0345 / 0.0290, 640x480 0.0220 / 0.0203; D=64, 192, 256
+// keep theirs (the swapped set: 0.0650 -> 0.0667, 0.1287 -> 0.1319, 0.1494
+// -> 0.1646).  MFMA groups of 4 tiles: 2 / 6 / 12 within 0.5 % or slower.
+constexpr int kCensusCostPx4 = 64, kCensusCostPx8 = 64, kCensusCostPx12 = 64, kCensusCostPx16 = 128;
 // Cost-volume stores of census_cost: 1 non-temporal, 0 default policy.
 // Round 4, every width, on the VALU kernel
 // (profiles/r04_v3/ab_store_policy_all.log.txt, frame ms nt / default):
