@@ -149,6 +149,8 @@ constexpr int kCensusCostMinD = 64;
 // profiles/r01_v8/ab_census_cost_tiling.jsonl.)
 constexpr int kCensusCostRows = 8;
 constexpr int kCensusCostRowsSmall = 4;
+// (900 instead: within noise at 960x540 D=64 / 128, 0.0224 / 0.0293 vs 0.0223 /
+// 0.0289 ms, profiles/r04_v4/ab_census_cost_store_threshold.log.txt)
 constexpr int kCensusCostMinGroups = 1536;   // 6 per CU
 // census_cost_mma_kernel: pixels per workgroup row at D = 64 / 128 / 192 /
 // 256.  64 px hold 5 / 4 / 3 workgroups per CU where 128 px hold 4 / 3 / 2 /
@@ -172,6 +174,9 @@ constexpr int kCensusCostPx4 = 64, kCensusCostPx8 = 64, kCensusCostPx12 = 64, kC
 // 3.775 / 3.793, 4K D=192 6.042 / 6.078.  The MFMA kernel stages each row
 // and stores whole 128-byte lines, nt (single 4-byte nt stores from the MFMA
 // lanes: census_cost 0.57 ms at 1080p D=128, ab_census_cost_mfma.log.txt).
+// Re-checked on the re-tiled MFMA kernel, frame ms nt / default
+// (ab_census_cost_store_threshold.log.txt): 1080p D=128 0.9025 / 0.9215, D=256
+// 1.733 / 1.753, 4K D=256 7.59 / 7.64.
 constexpr int kCostStoreNT = 1;
 
 // ---- refpath.hip, Mode R plane kernel v3 ------------------
