@@ -80,8 +80,12 @@ def parse():
                          "if they fail; 'committed' reads the committed file only")
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--mode-r-only", action="store_true",
-                    help="run only three GPU Mode R frames (1080p pair 12->11, k=20) and exit: "
-                         "the child of the Mode R VALU counter pass")
+                    help="run only three GPU Mode R frames (pair 12->11, k=20, at --mode-r-size) "
+                         "and exit: the child of the Mode R VALU counter pass")
+    ap.add_argument("--mode-r-size", default="1920x1080",
+                    help="WxH of the --mode-r-only frames: the parent passes the size of the "
+                         "frame it timed (mode_r_child_args), so the counters and the kernel "
+                         "time describe the same launch")
     ap.add_argument("--streams", type=int, default=0,
                     help="pairs of a step go round-robin to this many contexts, each with its "
                          "own HIP stream and workspaces, so pairs overlap (0 = auto: 2 when a "
@@ -196,20 +200,40 @@ def mode_r_beside(ctx, W, H, rows=24, k=20, reps=3):
                                       pyoracle.OCamera.make(*cams[11]), k=k, mask=mask)
     cdt = time.perf_counter() - t0
     g, c = n_cand / gdt / 1e6, ncpu / cdt / 1e6
+    sample = (f"oracle/refpath_oracle.c svo_ref_pair, {W}x{H} pair 12->11 k={k}: a bounded "
+              f"sample of {rows} of the frame's {H} rows (the middle band, masked), "
+              f"{ncpu} candidates, {cdt:.2f} s; the rate is per candidate SAD, so it does "
+              "not depend on how many rows the sample holds")
     return {"unit": "Mcandidate-SADs/s", "gpu": round(g, 1), "gpu_ms_per_frame": round(gdt * 1e3, 3),
+            "W": W, "H": H,
             "ref_match_kernel_ms": round(km / kn, 4) if kn else None,
-            "cpu": round(c, 3), "cores": 1, "kind": "port",
-            "sample": f"oracle/refpath_oracle.c svo_ref_pair, {W}x{H} pair 12->11 k={k}: "
-                      f"{rows} rows, {ncpu} candidates, {cdt:.2f} s",
+            "cpu": round(c, 3), "cores": 1, "kind": "port", "sample": sample,
+            "cpu_baseline": {"value": round(c, 3), "unit": "Mcandidate-SADs/s", "cores": 1,
+                             "kind": "port", "sample": sample},
             "gpu_over_cpu": round(g / c, 1)}
 
 
-def mode_r_only():
-    """Three GPU Mode R frames of mode_r_beside's workload (the PMC child)."""
+def mode_r_child_args(W, H):
+    """Arguments of the Mode R PMC child: the frame size mode_r_beside timed."""
+    return ["--mode-r-only", "--mode-r-size", f"{int(W)}x{int(H)}"]
+
+
+def parse_size(s):
+    W, H = (int(v) for v in s.lower().split("x"))
+    if W <= 0 or H <= 0:
+        raise ValueError(f"bad frame size {s!r}")
+    return W, H
+
+
+def mode_r_only(size="1920x1080"):
+    """Three GPU Mode R frames of mode_r_beside's workload (the PMC child).
+    Writes the frame size it ran to $SVA_MODE_R_STAMP, so that the parent can
+    refuse counters taken on a different frame."""
     import torch
     import stereovisionarray_amd as sva
     from stereovisionarray_amd import synth
-    W, H, k = 1920, 1080, 20
+    W, H = parse_size(size)
+    k = 20
     cams = synth.reference_array(0.036 / W)
     cr, co = sva.Camera.make(*cams[12]), sva.Camera.make(*cams[11])
     ref = synth.texture(H, W, 5)
@@ -223,6 +247,10 @@ def mode_r_only():
                             d8.data_ptr())
     torch.cuda.synchronize()
     ctx.close()
+    stamp = os.environ.get("SVA_MODE_R_STAMP")
+    if stamp:
+        with open(stamp, "w") as f:
+            json.dump({"W": W, "H": H, "k": k}, f)
 
 
 def mode_r_roofline(mr):
@@ -230,10 +258,18 @@ def mode_r_roofline(mr):
     VALU issue rate: SQ_INSTS_VALU x 4 cycles (one wave64 VALU instruction
     occupies a SIMD for 4 cycles) / (1,024 SIMDs x clock x kernel time), the
     instructions from one live rocprofv3 pass over mode_r_only(), the kernel
-    time from the hipEvent-timed ref_match launches of mode_r_beside."""
+    time from the hipEvent-timed ref_match launches of mode_r_beside.  The
+    child runs mr's own frame size and stamps it; a mismatch is refused, so
+    the fraction never divides one frame's instructions by another's time."""
     import tempfile
     outdir = tempfile.mkdtemp(prefix="sva_pmc_r_", dir="/tmp")
-    res = _pmc_pass("SQ_INSTS_VALU GRBM_GUI_ACTIVE", [], outdir, child=["--mode-r-only"])
+    stamp = os.path.join(outdir, "mode_r_stamp.json")
+    res = _pmc_pass("SQ_INSTS_VALU GRBM_GUI_ACTIVE", [], outdir,
+                    child=mode_r_child_args(mr["W"], mr["H"]), env={"SVA_MODE_R_STAMP": stamp})
+    with open(stamp) as f:
+        ran = json.load(f)
+    if (ran["W"], ran["H"]) != (mr["W"], mr["H"]):
+        raise RuntimeError(f"Mode R PMC child ran {ran['W']}x{ran['H']}, timed {mr['W']}x{mr['H']}")
     c = res.get("ref_match", {})
     insts = c.get("SQ_INSTS_VALU")
     t_ms = mr.get("ref_match_kernel_ms")
@@ -241,6 +277,7 @@ def mode_r_roofline(mr):
         raise RuntimeError("no ref_plane3_kernel counters")
     cap = SIMDS * MI355X_ENGINE_GHZ * 1e9 * t_ms * 1e-3 / 4.0   # wave-instructions
     return {"bound": "valu", "unit": "wave-instructions", "kernel": "ref_plane3_kernel<20>",
+            "frame": f"{mr['W']}x{mr['H']}",
             "sq_insts_valu": int(insts), "kernel_ms": t_ms,
             "achieved_per_s": round(insts / (t_ms * 1e-3), 1),
             "peak_per_s": round(SIMDS * MI355X_ENGINE_GHZ * 1e9 / 4.0, 1),
@@ -328,7 +365,7 @@ MI355X_ENGINE_GHZ = 2.4   # peak engine clock (MI355X_MICROARCH.md)
 SIMDS = 1024              # 256 CUs x 4 SIMDs
 
 
-def _pmc_pass(counter, args, outdir, child=None):
+def _pmc_pass(counter, args, outdir, child=None, env=None):
     """One rocprofv3 PMC pass (one counter group, kernel trace only) over a short
     run of this bench as a CHILD process; returns {timer name: mean counter per
     launch} (several counters: {timer name: {counter: mean}})."""
@@ -343,7 +380,7 @@ def _pmc_pass(counter, args, outdir, child=None):
     cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc"] + counters + ["--kernel-trace",
            "-d", d, "-o", "run", "--output-format", "csv", "--",
            sys.executable, os.path.abspath(__file__)] + child
-    env = dict(os.environ, TMPDIR="/tmp", SVA_BENCH_PMC_CHILD="1")
+    env = dict(os.environ, TMPDIR="/tmp", SVA_BENCH_PMC_CHILD="1", **(env or {}))
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=170)
     if r.returncode != 0:
         raise RuntimeError(f"rocprofv3 --pmc {counter} exited {r.returncode}: {r.stderr[-300:]}")
@@ -371,6 +408,8 @@ def live_traffic(a):
     import tempfile
     outdir = tempfile.mkdtemp(prefix="sva_pmc_", dir="/tmp")
     args = ["--workload", a.workload, "--pairs-per-rank", str(a.pairs_per_rank)]
+    if getattr(a, "batch", False):
+        args.append("--batch")     # per-launch bytes of the batched launches the line grades
     fetch = _pmc_pass("FETCH_SIZE", args, outdir)
     write = _pmc_pass("WRITE_SIZE", args, outdir)
     out = {}
@@ -555,7 +594,9 @@ def roofline_of(kernels, W, H, D, workload, overlapped=False, frames_per_launch=
     achieved = alg_bytes / (agg["avg_ms"] * 1e-3) / 1e9
     out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-           "traffic": load_traffic(workload, name),
+           # the committed PMC file holds single-frame launches: a batched launch
+           # (frames_per_launch > 1) gets its traffic from the live passes only
+           "traffic": load_traffic(workload, name) if frames_per_launch == 1 else None,
            "kernel": name, "kernel_avg_ms": round(agg["avg_ms"], 4),
            "alg_bytes_per_launch": alg_bytes, "model": model}
     if overlapped:
@@ -591,7 +632,8 @@ def aggregation_roofline_of(kernels, W, H, D, traffic_per_kernel=None, overlappe
            "sum_ms": round(ms, 4), "alg_bytes_per_launch": alg,
            "model": "SURVEY §8d aggregation 10 B/disp + WTA 2 B/disp + 2 B/px, "
                     "sgm_paths + wta_hv timed-region averages"}
-    if traffic_per_kernel and all(k in traffic_per_kernel for k in AGG_KERNELS):
+    if traffic_per_kernel and all(k in traffic_per_kernel for k in AGG_KERNELS) \
+            and frames_per_launch == 1:      # committed bytes are single-frame launches
         out["traffic"] = sum(traffic_per_kernel[k]["hbm_bytes_per_launch"] for k in AGG_KERNELS)
         out["traffic_over_alg"] = round(out["traffic"] / alg, 3)
     if overlapped:
@@ -1079,7 +1121,7 @@ def main():
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
     if a.mode_r_only:
-        return mode_r_only()
+        return mode_r_only(a.mode_r_size)
     if mode == "engine":
         return run_engine(a, WORKLOADS[a.workload])
     world = int(os.environ.get("WORLD_SIZE", "1"))

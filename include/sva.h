@@ -165,9 +165,12 @@ int sva_census_d(void* ctx, const uint8_t* img, int width, int height, size_t pi
                  uint64_t* census);
 int sva_cost_d(void* ctx, const uint64_t* census_l, const uint64_t* census_r, int width,
                int height, const sva_sgm_params* p, uint8_t* C);
-/* Census of both images and the cost volume in one kernel (1-D steps,
- * dir_y = 0; the kernel sva_disparity_sgm* runs for every 1-D step).  Same
- * C bytes as sva_census_d x2 -> sva_cost_d; the census maps stay on chip. */
+/* Census of both images and the cost volume in one kernel, the one
+ * sva_disparity_sgm* runs: 1-D steps (dir_y = 0), and 2-D steps whose
+ * primitive form has |dir_y| = 1 and |dir| <= 3 (every baseline of the
+ * reference's 5x5 rig, functions.cpp:148-213, and of a 2x4 grid); other
+ * steps return SVA_ERR_UNSUPPORTED.  Same C bytes as sva_census_d x2 ->
+ * sva_cost_d; the census maps stay on chip. */
 int sva_census_cost_d(void* ctx, const uint8_t* left, const uint8_t* right, int width,
                       int height, size_t pitch, const sva_sgm_params* p, uint8_t* C);
 int sva_paths_d(void* ctx, const uint8_t* C, int width, int height, const sva_sgm_params* p,

@@ -257,6 +257,25 @@ int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int
         }
         return SVA_OK;
     }
+    if (census_cost2_supported(Dp, p->dir, p->dir_y)) {
+        // 2-D array steps with |by| = 1 (every rig baseline of getCameraPairs
+        // and of BASELINE config 4): census + cost on the matrix cores in one
+        // kernel (census_cost2.hip)
+        SVA_HIP(c, launch_census_cost2(*c, left, right, W, H, pitch, Dp, p->dmin, p->dir,
+                                       p->dir_y, C, p->D),
+                "cost launch");
+        if ((s = paths_wta(c, C, W, H, p, Dp, disp, sub))) return s;
+        if (p->lr_check) {
+            SVA_HIP(c, launch_census_cost2(*c, right, left, W, H, pitch, Dp, p->dmin, -p->dir,
+                                           -p->dir_y, C, p->D),
+                    "cost launch");
+            if ((s = paths_wta(c, C, W, H, p, Dp, dr, nullptr))) return s;
+            SVA_HIP(c, launch_lr_check(*c, disp, dr, sub, W, H, p->dir, p->dir_y, p->lr_max_diff,
+                                       p->invalid),
+                    "lr launch");
+        }
+        return SVA_OK;
+    }
     SVA_HIP(c, c->census_l.ensure(np * 8), "census workspace");
     SVA_HIP(c, c->census_r.ensure(np * 8), "census workspace");
     uint64_t* cl = (uint64_t*)c->census_l.ptr;
@@ -324,6 +343,9 @@ int run_sgm_batch(Ctx* c, const sva_pair_d* jobs, int n, int W, int H, size_t pi
         if (q->dir_y == 0 && Dp >= tune::kCensusCostMinD && census_cost_supported(Dp)) {
             e = launch_census_cost(*c, jobs[i].left, jobs[i].right, W, H, pitch, Dp, q->dmin, q->dir,
                                    Ci, q->D);
+        } else if (census_cost2_supported(Dp, q->dir, q->dir_y)) {
+            e = launch_census_cost2(*c, jobs[i].left, jobs[i].right, W, H, pitch, Dp, q->dmin,
+                                    q->dir, q->dir_y, Ci, q->D);
         } else {
             uint64_t* cl = (uint64_t*)c->census_side.ptr + (size_t)(i % ns) * 2 * np;
             uint64_t* cr = cl + np;
@@ -707,9 +729,16 @@ int sva_census_cost_d(void* ctx, const uint8_t* left, const uint8_t* right, int 
     if ((s = check_image(c, left, W, H, pitch))) return s;
     if ((s = check_image(c, right, W, H, pitch))) return s;
     if (!C) return fail(c, SVA_ERR_INVALID_ARG, "null cost output");
-    if (p->dir_y != 0 || !census_cost_supported(p->D))
-        return fail(c, SVA_ERR_UNSUPPORTED, "census+cost kernel: 1-D steps, D in {64,128,192,256}");
-    SVA_HIP(c, launch_census_cost(*c, left, right, W, H, pitch, p->D, p->dmin, p->dir, C),
+    if (p->dir_y == 0 && census_cost_supported(p->D)) {
+        SVA_HIP(c, launch_census_cost(*c, left, right, W, H, pitch, p->D, p->dmin, p->dir, C),
+                "cost launch");
+        return SVA_OK;
+    }
+    if (!census_cost2_supported(p->D, p->dir, p->dir_y))
+        return fail(c, SVA_ERR_UNSUPPORTED,
+                    "census+cost kernel: D in {64,128,192,256}, 1-D steps or 2-D steps whose "
+                    "primitive form has |dir_y| = 1 and |dir| <= 3");
+    SVA_HIP(c, launch_census_cost2(*c, left, right, W, H, pitch, p->D, p->dmin, p->dir, p->dir_y, C),
             "cost launch");
     return SVA_OK;
 }

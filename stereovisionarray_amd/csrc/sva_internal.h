@@ -140,6 +140,12 @@ bool census_cost_supported(int D);
 // disparity count: d >= dreal gets cost 255 (0 = D).
 hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right, int W, int H,
                               size_t pitch, int D, int dmin, int dir, uint8_t* C, int dreal = 0);
+// Census + cost in one kernel for 2-D steps (census_cost2.hip): steps whose
+// primitive form has |by| = 1 and |bx| <= 3, native D.
+bool census_cost2_supported(int D, int sx, int sy);
+hipError_t launch_census_cost2(Ctx& c, const uint8_t* left, const uint8_t* right, int W, int H,
+                               size_t pitch, int D, int dmin, int sx, int sy, uint8_t* C,
+                               int dreal = 0);
 hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, int H, int D,
                        int dmin, int dir, uint8_t* C, int dreal = 0);
 // sgm_paths.hip -- all 8 directions in one launch.  CK == CKV == nullptr:

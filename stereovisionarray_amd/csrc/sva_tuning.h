@@ -178,6 +178,9 @@ constexpr int kCensusCostPx4 = 64, kCensusCostPx8 = 64, kCensusCostPx12 = 64, kC
 // (ab_census_cost_store_threshold.log.txt): 1080p D=128 0.9025 / 0.9215, D=256
 // 1.733 / 1.753, 4K D=256 7.59 / 7.64.
 constexpr int kCostStoreNT = 1;
+// census_cost2.hip (2-D array steps): adjacent lattice lines per workgroup,
+// which share one staged image patch.
+constexpr int kCensusCost2Lines = 8;
 
 // ---- refpath.hip, Mode R plane kernel v3 ------------------
 constexpr int kPlaneOuKB = 24;      // staged O chunk (KB)

@@ -102,20 +102,65 @@ def test_aggregation_roofline(bench, monkeypatch):
     assert out["aggregation_roofline"]["traffic"] == 7
 
 
+def fake_mode_r_pass(seen, ran=None):
+    """A stand-in PMC pass that records the child's arguments and stamps the
+    frame size the child would have run (or `ran`)."""
+    import json
+
+    def fake(counter, args, outdir, child=None, env=None):
+        seen["counter"], seen["child"] = counter, child
+        i = child.index("--mode-r-size")
+        W, H = (int(v) for v in (ran or child[i + 1]).split("x"))
+        with open(env["SVA_MODE_R_STAMP"], "w") as f:
+            json.dump({"W": W, "H": H, "k": 20}, f)
+        return {"ref_match": {"SQ_INSTS_VALU": 300e6, "GRBM_GUI_ACTIVE": 2.0e6}}
+    return fake
+
+
 def test_mode_r_valu_roofline(bench, monkeypatch):
     """VERDICT r03 next #5: SQ_INSTS_VALU x 4 / (1024 SIMDs x 2.4 GHz x kernel time)."""
     seen = {}
-
-    def fake(counter, args, outdir, child=None):
-        seen["counter"], seen["child"] = counter, child
-        return {"ref_match": {"SQ_INSTS_VALU": 300e6, "GRBM_GUI_ACTIVE": 2.0e6}}
-    monkeypatch.setattr(bench, "_pmc_pass", fake)
-    rf = bench.mode_r_roofline({"ref_match_kernel_ms": 0.8})
-    assert seen["counter"] == "SQ_INSTS_VALU GRBM_GUI_ACTIVE" and seen["child"] == ["--mode-r-only"]
+    monkeypatch.setattr(bench, "_pmc_pass", fake_mode_r_pass(seen))
+    rf = bench.mode_r_roofline({"ref_match_kernel_ms": 0.8, "W": 1920, "H": 1080})
+    assert seen["counter"] == "SQ_INSTS_VALU GRBM_GUI_ACTIVE"
+    assert seen["child"] == ["--mode-r-only", "--mode-r-size", "1920x1080"]
     assert abs(rf["frac"] - 300e6 * 4 / (1024 * 2.4e9 * 0.8e-3)) < 1e-4
     assert rf["bound"] == "valu" and rf["sq_insts_valu"] == 300000000
+    assert rf["frame"] == "1920x1080"
     with pytest.raises(RuntimeError):
-        bench.mode_r_roofline({"ref_match_kernel_ms": None})
+        bench.mode_r_roofline({"ref_match_kernel_ms": None, "W": 1920, "H": 1080})
+
+
+def test_mode_r_child_runs_the_timed_frame(bench, monkeypatch):
+    """VERDICT r04 next #1: the PMC child gets the timed frame's W and H (the
+    4K line once divided 1080p instruction counts by the 4K kernel time), and
+    a child that ran another size is refused."""
+    seen = {}
+    monkeypatch.setattr(bench, "_pmc_pass", fake_mode_r_pass(seen))
+    rf = bench.mode_r_roofline({"ref_match_kernel_ms": 4.7, "W": 3840, "H": 2160})
+    assert seen["child"] == ["--mode-r-only", "--mode-r-size", "3840x2160"]
+    assert rf["frame"] == "3840x2160"
+    monkeypatch.setattr(bench, "_pmc_pass", fake_mode_r_pass(seen, ran="1920x1080"))
+    with pytest.raises(RuntimeError, match="ran 1920x1080, timed 3840x2160"):
+        bench.mode_r_roofline({"ref_match_kernel_ms": 4.7, "W": 3840, "H": 2160})
+    assert bench.parse_size("3840x2160") == (3840, 2160)
+    with pytest.raises(ValueError):
+        bench.parse_size("0x10")
+
+
+def test_batched_launch_gets_no_single_frame_traffic(bench):
+    """ADVICE r04: a batched launch covers frames_per_launch frames, so the
+    committed single-frame PMC bytes must not be set against its algorithmic
+    bytes (that once reported traffic below the algorithmic minimum)."""
+    k = {"sgm_paths": {"avg_ms": 4.0}, "wta_hv": {"avg_ms": 2.0}}
+    rf = bench.roofline_of(k, 1920, 1080, 128, "1080p_d128", frames_per_launch=8)
+    assert rf["traffic"] is None and rf["frames_per_launch"] == 8
+    assert rf["alg_bytes_per_launch"] == 10.0 * 1920 * 1080 * 128 * 8
+    committed = {"sgm_paths": {"hbm_bytes_per_launch": 3}, "wta_hv": {"hbm_bytes_per_launch": 4}}
+    ag = bench.aggregation_roofline_of(k, 1920, 1080, 128, committed, frames_per_launch=8)
+    assert ag["traffic"] is None
+    ag1 = bench.aggregation_roofline_of(k, 1920, 1080, 128, committed)
+    assert ag1["traffic"] == 7
 
 
 def mode_args(**kw):

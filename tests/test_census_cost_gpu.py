@@ -1,11 +1,13 @@
 """The census+cost kernel (census_cost.hip, sva_census_cost_d) vs the CPU
 oracle's census -> cost, bit-exact, and the pipelines that use it.
 
-The kernel serves sva_disparity_sgm* for 1-D steps without the L/R check, so
-these cases cover its tiling edges: widths that are not a multiple of its
-128-pixel tile, heights below the 7-row window and not a multiple of its
-row band, large dmin (every matched column outside the image), both step
-signs, pitched images, and all four D.
+The kernel serves sva_disparity_sgm* for every 1-D step, so these cases
+cover its tiling edges: widths that are not a multiple of its pixel tile (64
+pixels at D = 64/128/192, 128 at D = 256: tune::kCensusCostPx*), heights
+below the 7-row window and not a multiple of its row band (8 rows where the
+grid keeps >= 1536 workgroups, else 4), large dmin (every matched column
+outside the image), both step signs, pitched images, and all four D.  The
+2-D array steps have their own kernel (test_census_cost2_gpu.py).
 """
 import numpy as np
 import pytest
@@ -115,15 +117,18 @@ def test_census_cost_matches_split_kernels(ctx, sva, torch_dev, D, dir, dmin):
     assert torch.equal(C1, C2)
 
 
-def test_census_cost_rejects_2d_steps(ctx, sva, torch_dev):
-    W, H = 64, 16
-    img = torch.zeros((H, W), dtype=torch.uint8, device=torch_dev)
-    C = torch.zeros((H, W, 64), dtype=torch.uint8, device=torch_dev)
-    p = sva.default_params(D=64)
-    p.dir, p.dir_y = 0, 1
-    with pytest.raises(sva.SvaError) as e:
-        ctx.census_cost_d(img.data_ptr(), img.data_ptr(), W, H, W, p, C.data_ptr())
-    assert e.value.status == sva.SVA_ERR_UNSUPPORTED
+@pytest.mark.parametrize("dir", [-1, 1])
+def test_census_cost_8_row_partial_band(ctx, sva, oracle, torch_dev, dir):
+    """a frame large enough for the 8-row bands (>= 1536
+    workgroups) whose height is not a multiple of 8, so the last band is
+    partial in 8-row mode (1920 x 1077: 30 x 135 workgroups, 5 rows in the
+    last band)."""
+    W, H, D = 1920, 1077, 128
+    L, R, _ = synth.stereo_pair(H, W, D, 0, dir, seed=77)
+    got = cost_gpu(ctx, sva, L, R, D, 0, dir, torch_dev)
+    want = oracle.cost(oracle.census(L), oracle.census(R), D, 0, dir)
+    assert np.array_equal(got[-16:], want[-16:])
+    assert np.array_equal(got, want)
 
 
 @pytest.mark.parametrize("D,dir,dmin", [(64, 1, 3), (128, -1, 0), (192, -1, 5), (256, 1, 0)])
