@@ -107,6 +107,16 @@ constexpr int kWtahvPinWta = 1;
 // -> 0.2495 / 0.2450 ms, D=64 0.150 -> 0.144, D=192 0.393 -> 0.380, D=256
 // 0.556 -> 0.538, 4K D=256 2.215 -> 2.158.
 constexpr int kWtahvSubLds = 1;
+// Round 5 (wta_hv VALU).  kWtahvKeyPerm: the WTA keys
+// (S << 16 | d) built with one v_perm per half from a per-lane disparity
+// pair register, 2 VALU per pair instead of 4.  kWtahvSubDeferred: the
+// owning lane reads S(d*-1), S(d*+1) of its pixel once after the row
+// segment (every pixel's S stays in its own LDS block), instead of an
+// exec-masked read block per pixel.
+constexpr int kWtahvKeyPerm = 1;
+constexpr int kWtahvSubDeferred = 1;
+// Minimum waves per SIMD asked of the compiler for wta_hv (launch bounds).
+constexpr int kWtahvMinWaves = 1;
 // LDS V blocks at D = 256 (8 u16 pairs = two 16-byte chunks per lane): 1 swaps
 // a lane's two chunks when ((k >> 2) ^ (k >> 3)) & 1, which makes every
 // ds_write_b128 (8-lane groups, 32 banks) and ds_read_b128 (16-lane groups

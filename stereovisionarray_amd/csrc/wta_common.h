@@ -86,6 +86,27 @@ __device__ __forceinline__ unsigned wta_pick_key(const unsigned (&S)[DPL / 2], i
     return row_min_u32<PIN>(best);
 }
 
+// The same key with each pair's two keys formed by one v_perm each: dpair[j]
+// holds the pair's disparities (d0 + 2j) | (d0 + 2j + 1) << 16, so the key of
+// the low half is [dpair.lo16 | S.lo16 << 16] and of the high half
+// [dpair.hi16 | S.hi16 << 16]: 2 VALU per pair where the shift/mask + or
+// forms took 4.
+template <int DPL, bool PIN = false>
+__device__ __forceinline__ unsigned wta_pick_key_perm(const unsigned (&S)[DPL / 2],
+                                                      const unsigned (&dpair)[DPL / 2]) {
+    constexpr int NP = DPL / 2;
+    unsigned key[2 * NP];
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+        key[2 * j] = __builtin_amdgcn_perm(S[j], dpair[j], 0x05040100u);
+        key[2 * j + 1] = __builtin_amdgcn_perm(S[j], dpair[j], 0x07060302u);
+    }
+    unsigned best = key[0];
+#pragma unroll
+    for (int i = 1; i < 2 * NP; i++) best = best < key[i] ? best : key[i];
+    return row_min_u32<PIN>(best);
+}
+
 // Returns d* (0-based, the same in all 16 lanes of the row) and, when
 // want_sub, the f32 sub-pixel disparity dmin + d* (+ parabola offset) in *v.
 template <int DPL>

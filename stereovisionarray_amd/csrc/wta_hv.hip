@@ -52,7 +52,7 @@ template <int DPL> constexpr int pf_vol() {
 }
 
 template <int DPL, int TYL, bool PAD>
-__global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ C,
+__global__ __launch_bounds__(TB, tune::kWtahvMinWaves) void wta_hv_kernel(const uint8_t* __restrict__ C,
                                                     const uint8_t* __restrict__ L4,
                                                     const uint8_t* __restrict__ CK,
                                                     const uint8_t* __restrict__ CKV, WtaHvGeom g,
@@ -357,12 +357,17 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
     else zero_state(Aa, ma);
     unsigned dres = 0u, sm = 0u, s0 = 0u;
     const bool want_sub = sub != nullptr;
+    unsigned dpair[NP];                                // (d, d + 1) of each pair (kWtahvKeyPerm)
+#pragma unroll
+    for (int j = 0; j < NP; j++) dpair[j] = (lane_d + 2u * j) | ((lane_d + 2u * j + 1u) << 16);
+    constexpr bool DEFER = tune::kWtahvSubLds != 0 && tune::kWtahvSubDeferred != 0;
+    unsigned* const vrow = &vsum[(hr * TW + hseg * TY) * 16 * NP];   // the segment's V blocks
     for_seq<TY>([&](auto Q) {
         constexpr int q = decltype(Q)::value, j = TY - 1 - q, s = q % kPfVol;
         if (j < nh) {
             unsigned ow[NW];
             sgm_step<DPL, PIN>(ch[j].w, Aa, ma, ow, P1, P2, ea);
-            unsigned* const vpix = &vsum[(hr * TW + hseg * TY + j) * 16 * NP];   // this pixel's V
+            unsigned* const vpix = vrow + j * 16 * NP;                     // this pixel's V
             unsigned S[NP];
 #pragma unroll
             for (int p = 0; p < NP; p++) S[p] = vpix[vw(p)] + Aa[p];   // V + L_1
@@ -384,19 +389,26 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
                 // pairs over the pixel's V block, which nothing reads again;
                 // as u16 the block is S indexed by d (up to the swizzle).  The owning lane reads
                 // the two neighbours (same wave, behind a wave barrier).
-                const unsigned best = wta_pick_key<DPL, PIN && tune::kWtahvPinWta>(S, k);
+                const unsigned best = tune::kWtahvKeyPerm
+                                          ? wta_pick_key_perm<DPL, PIN && tune::kWtahvPinWta>(S, dpair)
+                                          : wta_pick_key<DPL, PIN && tune::kWtahvPinWta>(S, k);
                 const int ds = (int)(best & 0xffffu);
                 if (want_sub) {
 #pragma unroll
                     for (int p = 0; p < NP; p++) vpix[vw(p)] = S[p];
-                    // the owning lane reads what other lanes of this wave just
-                    // wrote: state the ordering (a wave's LDS operations
-                    // execute in issue order, so this costs no instruction)
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if constexpr (!DEFER) {
+                        // the owning lane reads what other lanes of this wave just
+                        // wrote: state the ordering (a wave's LDS operations
+                        // execute in issue order, so this costs no instruction)
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    }
                 }
-                if (k == j) {
+                if constexpr (DEFER) {
+                    dres = k == j ? (unsigned)ds : dres;
+                    s0 = k == j ? best >> 16 : s0;
+                } else if (k == j) {
                     dres = (unsigned)ds;
                     s0 = best >> 16;
                     if (want_sub) {
@@ -425,6 +437,25 @@ __global__ __launch_bounds__(TB) void wta_hv_kernel(const uint8_t* __restrict__ 
             __builtin_amdgcn_sched_barrier(0);
         }
     });
+    if constexpr (DEFER) {
+        // S(d*-1), S(d*+1) of lane k's pixel (j = k) from the S its row wrote
+        // over the pixel's V block (same wave: order, no barrier instruction)
+        if (want_sub) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (k < nh) {
+                const uint16_t* s16 = reinterpret_cast<const uint16_t*>(vrow + k * 16 * NP);
+                const int ds = (int)dres;
+                const int dm = ds > 0 ? ds - 1 : 0, dp = ds + 1 < 16 * DPL ? ds + 1 : ds;
+                auto at = [&](int d) {
+                    const int kk = d / DPL, pp = (d >> 1) % NP;
+                    return (unsigned)s16[2 * (kk * NP + (pp ^ vsw_of(kk))) + (d & 1)];
+                };
+                sm = at(dm) | (at(dp) << 16);
+            }
+        }
+    }
     if (k < nh) {
         const size_t at = (size_t)yh * (size_t)W + (size_t)(hx + k);
         disp[at] = (uint16_t)(g.dmin + (int)dres);

@@ -6,7 +6,7 @@ stereovisionarray_amd/csrc with literal text replacements applied:
 
 Each OLD must occur in FILE (all occurrences are replaced); OLD = '@' copies
 the file at path NEW over FILE.  Output:
-ab_libs/libsva_NAME.so; the product sources and libsva.so are untouched.
+$AB_DIR/libsva_NAME.so (default ab_libs/); the product sources and libsva.so are untouched.
 Ablation builds compute other values on purpose (run tools/ab_paths.py with
 AB_NOCHECK=1)."""
 import os
@@ -34,10 +34,11 @@ def main():
         if old not in t:
             raise SystemExit(f"{f}: pattern not found: {old[:80]}")
         open(p, "w").write(t.replace(old, new))
-    os.makedirs(os.path.join(ROOT, "ab_libs"), exist_ok=True)
+    out = os.environ.get("AB_DIR", "ab_libs")      # ab_run/ for libraries a GPU run loads
+    os.makedirs(os.path.join(ROOT, out), exist_ok=True)
     subprocess.run(["make", "-s", "-j8", "-C", src, f"BUILD={ROOT}/build/var_{name}/obj",
-                    f"OUT={ROOT}/ab_libs/libsva_{name}.so", f"INC={ROOT}/include"], check=True)
-    print(f"built ab_libs/libsva_{name}.so")
+                    f"OUT={ROOT}/{out}/libsva_{name}.so", f"INC={ROOT}/include"], check=True)
+    print(f"built {out}/libsva_{name}.so")
 
 
 if __name__ == "__main__":

@@ -5,10 +5,12 @@
 # (build/var_<name>/src) whose sva_tuning.h has the named constexpr constants
 # rewritten; product translation units carry no experiment switches.  A value
 # may also be a whole replacement file: name "@path/to/tuning.h".
-# Output: ab_libs/libsva_<name>.so (the product libsva.so is untouched).
+# Output: $AB_DIR/libsva_<name>.so, default ab_libs/ (gpurun-ignored: set
+# AB_DIR=ab_run for libraries a GPU run loads).  The product libsva.so is untouched.
 set -eu
 cd "$(dirname "$0")/.."
-mkdir -p ab_libs
+AB=${AB_DIR:-ab_libs}
+mkdir -p "$AB"
 while [ $# -ge 2 ]; do
   name=$1 spec=$2; shift 2
   src=build/var_$name/src
@@ -23,7 +25,7 @@ while [ $# -ge 2 ]; do
       sed -i -E "s/\b($k) = [^,;]+/\1 = $v/" "$src/sva_tuning.h"
     done
   fi
-  make -s -j8 -C "$src" BUILD="$PWD/build/var_$name/obj" OUT="$PWD/ab_libs/libsva_$name.so" \
+  make -s -j8 -C "$src" BUILD="$PWD/build/var_$name/obj" OUT="$PWD/$AB/libsva_$name.so" \
        INC="$PWD/include"
-  echo "built ab_libs/libsva_$name.so ($spec)"
+  echo "built $AB/libsva_$name.so ($spec)"
 done
