@@ -615,7 +615,28 @@ def roofline_of(kernels, W, H, D, workload, overlapped=False, frames_per_launch=
 # timed-region hipEvent averages, so moving work between the two kernels
 # cannot move the grade.
 AGG_KERNELS = ("sgm_paths", "wta_hv")
-BATCH_MAX_PAIRS = 8    # frames per launch of sva_disparity_sgm_batch_d (sva_tuning.h)
+# sva_disparity_sgm_batch_d (sva_tuning.h): calls are split into chunks of at
+# most 8 frames, each aggregated in sub-batches of 4 frames per launch
+BATCH_MAX_PAIRS = 8
+BATCH_SUB_FRAMES = 4
+
+
+def batch_groups(n, groups):
+    """[j0, j1) of each of `groups` contiguous batch calls over n pairs."""
+    g = max(1, min(groups, n))
+    return [(n * i // g, n * (i + 1) // g) for i in range(g)] + [(n, n)] * (groups - g)
+
+
+def batch_frames_per_launch(n, groups=1):
+    """Mean frames per aggregation launch of `groups` batch calls over n pairs."""
+    launches = frames = 0
+    for j0, j1 in batch_groups(n, groups):
+        m = j1 - j0
+        for c0 in range(0, m, BATCH_MAX_PAIRS):
+            cm = min(BATCH_MAX_PAIRS, m - c0)
+            launches += -(-cm // BATCH_SUB_FRAMES)
+            frames += cm
+    return frames / launches if launches else 1
 
 
 def aggregation_roofline_of(kernels, W, H, D, traffic_per_kernel=None, overlapped=False,
@@ -721,8 +742,8 @@ def run_array(a, wl, world, rank, local, dev):
     # 311.2-315.0K (2) -> 319.7-321.0K (3) -> 309.3K (4) Mdisp/s; grid8_all
     # 316.2-316.9K (2) -> 316.4-318.1K (3) -> 305.2-308.1K (4).
     n_streams = a.streams if a.streams > 0 else (min(3, len(jobs)) if len(jobs) > 1 else 1)
-    if a.batch:
-        n_streams = 1                    # the batch runs on one context
+    if a.batch and a.streams <= 0:
+        n_streams = 1                    # the batch runs on one context (--streams S: S batches)
     ctxs, cstreams = [ctx], [stream]
     for _ in range(1, n_streams):
         s_ = torch.cuda.Stream(dev)
@@ -769,8 +790,11 @@ def run_array(a, wl, world, rank, local, dev):
             for s_ in cstreams[1:]:
                 s_.wait_event(go)
         if a.batch:
-            ctx.disparity_sgm_batch_d([(L.data_ptr(), R.data_ptr(), p) for (L, R, p) in jobs],
-                                      W, H, W, dsp.data_ptr())
+            # --streams S: the pairs in S contiguous groups, one batch call per context
+            for c_, (j0, j1) in zip(ctxs, batch_groups(len(jobs), len(ctxs))):
+                if j1 > j0:
+                    c_.disparity_sgm_batch_d([(L.data_ptr(), R.data_ptr(), p) for (L, R, p) in
+                                              jobs[j0:j1]], W, H, W, dsp[j0].data_ptr())
         else:
             for jb, (L, R, p) in enumerate(jobs):
                 ctxs[jb % len(ctxs)].disparity_sgm_d(L.data_ptr(), R.data_ptr(), W, H, W, p,
@@ -810,11 +834,7 @@ def run_array(a, wl, world, rank, local, dev):
     value = n_units * W * H * D * a.steps / elapsed / 1e6
     # committed PMC bytes per pair: the 1080p D=128 frame's for the 1080p rigs
     traffic_wl = "1080p_d128" if (W, H, D) == (1920, 1080, 128) else a.workload
-    if a.batch:   # frames per aggregation launch: the mean over this rank's launches
-        n_launch = -(-len(jobs) // BATCH_MAX_PAIRS)
-        fpl = len(jobs) / n_launch
-    else:
-        fpl = 1
+    fpl = batch_frames_per_launch(len(jobs), len(ctxs)) if a.batch else 1
     exchange = None
     if multi:
         def recompute(u):
@@ -1161,8 +1181,8 @@ def main():
     # two streams win there too: 304.9-307.7K -> 317.9K Mdisp/s
     # (profiles/r03_v8/streams_batch256.log.txt).
     n_streams = a.streams if a.streams > 0 else (1 if P == 1 else 2)
-    if a.batch:
-        n_streams = 1                    # the batch runs on one context
+    if a.batch and a.streams <= 0:
+        n_streams = 1                    # the batch runs on one context (--streams S: S batches)
     ctx = sva.Context(local)
     stream = torch.cuda.Stream(dev)     # non-default stream shared by kernels, copies, RCCL
     torch.cuda.set_stream(stream)
@@ -1220,7 +1240,10 @@ def main():
             for s_ in cstreams[1:]:
                 s_.wait_event(go)
         if a.batch:
-            ctx.disparity_sgm_batch_d(batch_jobs, W, H, W, disp.data_ptr(), sub.data_ptr())
+            for c_, (j0, j1) in zip(ctxs, batch_groups(P, len(ctxs))):
+                if j1 > j0:
+                    c_.disparity_sgm_batch_d(batch_jobs[j0:j1], W, H, W, disp[j0].data_ptr(),
+                                             sub[j0].data_ptr())
         else:
             for j in range(P):
                 ctxs[j % len(ctxs)].disparity_sgm_d(lefts[j].data_ptr(), rights[j].data_ptr(), W,
@@ -1269,7 +1292,7 @@ def main():
     disparities = units * W * H * D
     value = disparities / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1e3
-    fpl = P / -(-P // BATCH_MAX_PAIRS) if a.batch else 1
+    fpl = batch_frames_per_launch(P, len(ctxs)) if a.batch else 1
     roofline = roofline_of(kernels, W, H, D, a.workload, overlapped=len(ctxs) > 1,
                            frames_per_launch=fpl)
     out = {

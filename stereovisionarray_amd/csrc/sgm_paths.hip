@@ -27,13 +27,15 @@
 // Two output modes (g.ckpt):
 //   0  every direction writes its u8 volume, [8][H][W][D] (sva_paths_d, the
 //      stage API the parity tests read): 8 C reads + 8 L writes per disparity.
-//   2  the frame route, the tile pipeline: the up
-//      diagonals 5 and 7 write volumes, [2][H][W][D] (slots 0, 1); horizontal
-//      lines store checkpoints every seg columns ([2][H][nsx][D]), vertical
-//      and down-diagonal lines every seg rows ([4][nsy][W][D]: directions 2,
-//      3, 4, 6; seg = 2^tile_geom().seg_log2), and wta_hv.hip recomputes
-//      those six per tile: 8 C reads + 2 L writes.  (tune::kTileDiagDown =
-//      0: all four diagonals write volumes, [4][H][W][D], round 3.)
+//   2  the frame route, the tile pipeline: the four
+//      diagonal directions write volumes, [4][H][W][D] (directions 4..7 in
+//      slots 0..3); horizontal lines store checkpoints every seg columns
+//      ([2][H][nsx][D]) and vertical lines every seg rows ([2][nsy][W][D];
+//      seg = 2^tile_geom().seg_log2), and wta_hv.hip recomputes those four
+//      per tile: 8 C reads + 4 L writes.  (The measured §4.11 experiment,
+//      tune::kTileDiagDown / kTileDiagUp = 1, also recomputes a diagonal pair
+//      per tile from extra row-checkpoint planes; both constants are 0 in the
+//      product.)
 //   (Mode 1, the round-2 route of DESIGN.md §4.6 -- six volumes, horizontal
 //   checkpoints only, finished by wta_h.hip -- was removed in ABI v5.)
 #include "sgm_common.h"

@@ -296,11 +296,16 @@ int run_sgm_device(Ctx* c, const uint8_t* left, const uint8_t* right, int W, int
     return SVA_OK;
 }
 
-// A batch of frames of one shape through one launch of each aggregation
+// A batch of frames of one shape through few launches of each aggregation
 // kernel: the cost volume of every frame (census + cost per
-// frame, each along its own step), then sgm_paths and wta_hv once over all of
-// them.  jobs[0..n) share D, dmin, P1, P2 and subpixel (checked by the entry
-// point); maps / sub hold n planes of W*H.
+// frame, each along its own step), then sgm_paths and wta_hv once per
+// sub-batch of tune::kBatchSubFrames frames.  The frames' census + cost
+// kernels run on up to tune::kBatchCostStreams side streams forked from the
+// context stream, in frame order per stream; the context stream starts a
+// sub-batch's aggregation as soon as that sub-batch's costs are done, so the
+// next sub-batches' (VALU-bound, small) cost kernels overlap the current
+// (HBM-bound) aggregation.  jobs[0..n) share D, dmin, P1, P2 and subpixel
+// (checked by the entry point); maps / sub hold n planes of W*H.
 int run_sgm_batch(Ctx* c, const sva_pair_d* jobs, int n, int W, int H, size_t pitch,
                   uint16_t* maps, float* sub) {
     const sva_sgm_params* p = &jobs[0].params;
@@ -308,31 +313,32 @@ int run_sgm_batch(Ctx* c, const sva_pair_d* jobs, int n, int W, int H, size_t pi
     const size_t np = (size_t)W * H, nv = np * (size_t)Dp;
     const TileGeom tg = tile_geom(W, H, Dp);
     const size_t ckb = tg.hck_bytes + tg.vck_bytes + tg.dck_bytes;
+    const int sb = tune::kBatchSubFrames > 0 ? std::min(n, tune::kBatchSubFrames) : n;
+    const int nsub = (n + sb - 1) / sb;
     SVA_HIP(c, c->cost.ensure(nv * n), "cost workspace");
-    SVA_HIP(c, c->paths.ensure(nv * tg.nvol * n), "path workspace");
-    SVA_HIP(c, c->ckpt.ensure(ckb * n), "checkpoint workspace");
+    // the aggregation workspaces serve one sub-batch at a time (same stream)
+    SVA_HIP(c, c->paths.ensure(nv * tg.nvol * sb), "path workspace");
+    SVA_HIP(c, c->ckpt.ensure(ckb * sb), "checkpoint workspace");
     uint8_t* C = (uint8_t*)c->cost.ptr;
-    // The frames' census + cost kernels are VALU-bound and small: they run
-    // concurrently on up to tune::kBatchCostStreams side streams, forked from
-    // and joined back into the context stream.
     const int ns = std::min(n, tune::kBatchCostStreams);
     if (ns > 1) {
         while ((int)c->side.size() < ns) {
             hipStream_t s = nullptr;
-            hipEvent_t e = nullptr;
             SVA_HIP(c, hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "side stream");
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-                (void)hipStreamDestroy(s);
-                return fail(c, SVA_ERR_DEVICE, "side stream event");
-            }
             c->side.push_back(s);
+        }
+        // one event per (sub-batch, side stream): "this stream's frames of
+        // sub-batch j have their cost volumes"
+        while ((int)c->side_done.size() < ns * nsub) {
+            hipEvent_t e = nullptr;
+            SVA_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming), "side stream event");
             c->side_done.push_back(e);
         }
         if (!c->fork) SVA_HIP(c, hipEventCreateWithFlags(&c->fork, hipEventDisableTiming), "fork event");
         SVA_HIP(c, hipEventRecord(c->fork, c->stream), "fork");
         for (int s = 0; s < ns; s++) SVA_HIP(c, hipStreamWaitEvent(c->side[s], c->fork, 0), "fork");
     }
-    SVA_HIP(c, c->census_side.ensure(np * 16 * (size_t)ns), "census workspace");
+    SVA_HIP(c, c->census_side.ensure(np * 16 * (size_t)std::max(ns, 1)), "census workspace");
     const hipStream_t own = c->stream;
     int st = SVA_OK;
     for (int i = 0; i < n && st == SVA_OK; i++) {
@@ -347,31 +353,45 @@ int run_sgm_batch(Ctx* c, const sva_pair_d* jobs, int n, int W, int H, size_t pi
             e = launch_census_cost2(*c, jobs[i].left, jobs[i].right, W, H, pitch, Dp, q->dmin,
                                     q->dir, q->dir_y, Ci, q->D);
         } else {
-            uint64_t* cl = (uint64_t*)c->census_side.ptr + (size_t)(i % ns) * 2 * np;
+            uint64_t* cl = (uint64_t*)c->census_side.ptr + (size_t)(i % std::max(ns, 1)) * 2 * np;
             uint64_t* cr = cl + np;
             e = launch_census_pair(*c, jobs[i].left, jobs[i].right, W, H, pitch, cl, cr);
             if (e == hipSuccess)
                 e = launch_cost2(*c, cl, cr, W, H, Dp, q->dmin, q->dir, q->dir_y, Ci, q->D);
         }
+        // the last frame of a sub-batch on this side stream (or of the batch)
+        if (e == hipSuccess && ns > 1 && (i + ns >= n || (i + ns) / sb != i / sb))
+            e = hipEventRecord(c->side_done[(size_t)(i / sb) * ns + i % ns], c->stream);
         c->stream = own;
         if (e != hipSuccess) st = hip_fail(c, e, "cost launch");
     }
-    if (ns > 1) {   // join, also after a failed launch: the side streams stay ordered
-        for (int s = 0; s < ns; s++) {
-            SVA_HIP(c, hipEventRecord(c->side_done[s], c->side[s]), "join");
-            SVA_HIP(c, hipStreamWaitEvent(c->stream, c->side_done[s], 0), "join");
+    // Aggregation per sub-batch on the context stream, after its costs.  A
+    // failed cost launch still joins every side stream (they stay ordered).
+    for (int j = 0; j < nsub; j++) {
+        const int i0 = j * sb, m = std::min(sb, n - i0);
+        if (ns > 1) {
+            for (int s = 0; s < ns && s < n; s++) {
+                // side stream s holds frames of sub-batch j: its event recorded
+                // after the last of them
+                bool has = false;
+                for (int i = i0; i < i0 + m; i++) has = has || i % ns == s;
+                if (!has) continue;
+                SVA_HIP(c, hipStreamWaitEvent(c->stream, c->side_done[(size_t)j * ns + s], 0), "join");
+            }
         }
+        if (st) continue;
+        uint8_t* L4 = (uint8_t*)c->paths.ptr;
+        uint8_t* CK = (uint8_t*)c->ckpt.ptr;
+        // horizontal planes of the sub-batch's frames, then their vertical planes
+        uint8_t* CKV = CK + tg.hck_bytes * m;
+        const uint8_t* Cj = C + (size_t)i0 * nv;
+        SVA_HIP(c, launch_paths(*c, Cj, W, H, Dp, p->P1, p->P2, L4, CK, CKV, m), "paths launch");
+        SVA_HIP(c, launch_wta_hv(*c, Cj, L4, CK, CKV, W, H, Dp, p->P1, p->P2, p->dmin,
+                                 maps + (size_t)i0 * np,
+                                 p->subpixel ? sub + (size_t)i0 * np : nullptr, p->D, m),
+                "wta launch");
     }
-    if (st) return st;
-    uint8_t* L4 = (uint8_t*)c->paths.ptr;
-    uint8_t* CK = (uint8_t*)c->ckpt.ptr;
-    // horizontal planes of all frames, then vertical planes of all frames
-    uint8_t* CKV = CK + tg.hck_bytes * n;
-    SVA_HIP(c, launch_paths(*c, C, W, H, Dp, p->P1, p->P2, L4, CK, CKV, n), "paths launch");
-    SVA_HIP(c, launch_wta_hv(*c, C, L4, CK, CKV, W, H, Dp, p->P1, p->P2, p->dmin, maps,
-                             p->subpixel ? sub : nullptr, p->D, n),
-            "wta launch");
-    return SVA_OK;
+    return st;
 }
 
 int check_camera(Ctx* c, const sva_camera* cam) {

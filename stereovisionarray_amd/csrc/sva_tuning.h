@@ -138,6 +138,10 @@ constexpr int kBatchMaxPairs = 8;
 // context stream they were 36 % of a 960x540 D=64 center8 step,
 // profiles/r04_*/c8half_batch.log.txt).
 constexpr int kBatchCostStreams = 3;
+// Frames per aggregation launch inside a batch (0: the whole batch): the
+// context stream aggregates sub-batch j while the side streams compute the
+// cost volumes of sub-batch j + 1 (round 5).
+constexpr int kBatchSubFrames = 4;
 constexpr size_t kBatchMaxBytes = (size_t)24 << 30;
 
 // ---- census.hip / census_cost.hip / cost.hip ------------

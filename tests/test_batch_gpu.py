@@ -1,5 +1,7 @@
 """The batched frame route (sva_disparity_sgm_batch_d): n
-frames of one shape through one sgm_paths and one wta_hv launch.  Every
+frames of one shape through one sgm_paths and one wta_hv launch per sub-batch
+of tune::kBatchSubFrames frames, whose aggregation overlaps the next
+sub-batch's cost kernels on the side streams.  Every
 frame's map and sub-pixel map must equal the single-frame route's
 (sva_disparity_sgm_d) bit for bit, which the rest of the suite pins to the
 oracle; a few frames are checked against the oracle directly.  Frames differ
@@ -107,3 +109,38 @@ def test_batch_refuses_mixed_params(ctx, sva, torch_dev):
     with pytest.raises(sva.SvaError) as e:
         ctx.disparity_sgm_batch_d([], W, H, W, maps.data_ptr())
     assert e.value.status == sva.SVA_ERR_INVALID_ARG
+
+
+def test_batch_back_to_back_calls(ctx, sva, torch_dev):
+    """Two batch calls queued with no synchronisation between them (the second
+    call's side-stream cost kernels must not overwrite the first call's cost
+    volumes while its sub-batches aggregate), 9 frames each: sub-batches of
+    4 + 4 + 1 over three side streams."""
+    H, W, D = 36, 70, 64
+    fa = frames(H, W, D, 9, seed=31)
+    fb = frames(H, W, D, 9, seed=71)
+    dev_ = lambda a: torch.from_numpy(a).to(torch_dev)
+    calls = []
+    for fr in (fa, fb):
+        dl = [dev_(L) for L, _, _, _ in fr]
+        dr = [dev_(R) for _, R, _, _ in fr]
+        pairs = [(dl[i].data_ptr(), dr[i].data_ptr(),
+                  sva.default_params(D=D, dir=fr[i][2], dir_y=fr[i][3], subpixel=1))
+                 for i in range(len(fr))]
+        maps = torch.zeros((len(fr), H, W), dtype=torch.int16, device=torch_dev)
+        sub = torch.zeros((len(fr), H, W), dtype=torch.float32, device=torch_dev)
+        calls.append((fr, dl, dr, pairs, maps, sub))
+    for fr, dl, dr, pairs, maps, sub in calls:          # queued back to back
+        ctx.disparity_sgm_batch_d(pairs, W, H, W, maps.data_ptr(), sub.data_ptr())
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    one = torch.zeros((H, W), dtype=torch.int16, device=torch_dev)
+    one_sub = torch.zeros((H, W), dtype=torch.float32, device=torch_dev)
+    for fr, dl, dr, pairs, maps, sub in calls:
+        got, gsub = maps.cpu().numpy(), sub.cpu().numpy()
+        for i in range(len(fr)):
+            ctx.disparity_sgm_d(dl[i].data_ptr(), dr[i].data_ptr(), W, H, W, pairs[i][2],
+                                one.data_ptr(), one_sub.data_ptr())
+            ctx.synchronize()
+            assert np.array_equal(got[i], one.cpu().numpy()), i
+            assert np.array_equal(gsub[i].view(np.uint32), one_sub.cpu().numpy().view(np.uint32)), i
