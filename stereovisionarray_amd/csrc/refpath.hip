@@ -14,6 +14,7 @@
 #pragma clang fp contract(off)
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "sva_device.h"
 #include "sva_internal.h"
@@ -208,6 +209,34 @@ __device__ __forceinline__ unsigned scan64_dpp(unsigned v) {
     return v;
 }
 
+// The same scan on N pairs of values, stage by stage: each DPP add's source
+// was written 2N instructions earlier, so no s_nop separates dependent adds.
+template <int N>
+__device__ __forceinline__ void scan64_dpp_n(unsigned (&a)[N], unsigned (&b)[N]) {
+    auto stage = [&](auto ctl, int rmask) {
+        (void)rmask;
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            a[j] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)a[j], decltype(ctl)::value,
+                                                          decltype(ctl)::value >= 0x142
+                                                              ? (decltype(ctl)::value == 0x142 ? 0xa : 0xc)
+                                                              : 0xf,
+                                                          0xf, false);
+            b[j] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)b[j], decltype(ctl)::value,
+                                                          decltype(ctl)::value >= 0x142
+                                                              ? (decltype(ctl)::value == 0x142 ? 0xa : 0xc)
+                                                              : 0xf,
+                                                          0xf, false);
+        }
+    };
+    stage(std::integral_constant<int, 0x111>{}, 0xf);   // row_shr:1
+    stage(std::integral_constant<int, 0x112>{}, 0xf);   // row_shr:2
+    stage(std::integral_constant<int, 0x114>{}, 0xf);   // row_shr:4
+    stage(std::integral_constant<int, 0x118>{}, 0xf);   // row_shr:8
+    stage(std::integral_constant<int, 0x142>{}, 0xa);   // row_bcast:15 into rows 1, 3
+    stage(std::integral_constant<int, 0x143>{}, 0xc);   // row_bcast:31 into rows 2, 3
+}
+
 // ---- offset-plane algorithm (v3) ---------------------------------------------
 // The round-1 kernel (v2) spent most lanes on the window
 // halo: a wave covered the 64 region columns of a (64 - 2k)-pixel tile, so at
@@ -265,7 +294,12 @@ __device__ __forceinline__ void line_interval(int po, int pa, int pn, bool mi, b
             } else {
                 // i in [ceil((tt*b - mj)/a), ceil((tt*b + b - mj)/a)); the
                 // lower bound at tt = 0 is <= 0, i.e. 0 after clamping
-                const unsigned A = (unsigned)a;
+                // tune::kPlaneNoHoistDiv: an opaque copy keeps the compiler
+                // from hoisting each pixel's reciprocal of a out of the outer
+                // offset loop (no spill at k = 20, but the division is then
+                // redone per outer offset: +9 % on diagonal pairs)
+                unsigned A = (unsigned)a;
+                if constexpr (tune::kPlaneNoHoistDiv != 0) asm volatile("" : "+v"(A));
                 ilo = tt == 0 ? 0 : (int)(((unsigned)(tt * b - mj) + A - 1u) / A);
                 ihi = (int)(((unsigned)(tt * b + b - mj) + A - 1u) / A);
             }
@@ -414,7 +448,10 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
         for (int j = 0; j < 8; j++) {
             const int x = tx0 + lane, y = ty0 + r0 + j;
             const bool ok = (pn[j] & 0xffff) != 0;
-            const int4 rel = make_int4(E[j].x - x, E[j].y - y, E[j].z - x, E[j].w - y);
+            // the endpoints again from global memory (L2-hot): E[] need not
+            // stay live across the tile's box reduction and barrier
+            const int4 e = ends[(size_t)min(y, H - 1) * W + min(x, W - 1)];
+            const int4 rel = make_int4(e.x - x, e.y - y, e.z - x, e.w - y);
             const int lx = __shfl_up(rel.x, 1, 64), ly = __shfl_up(rel.y, 1, 64);
             const int lz = __shfl_up(rel.z, 1, 64), lw = __shfl_up(rel.w, 1, 64);
             const int lok = __shfl_up((int)ok, 1, 64);
@@ -490,6 +527,7 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
 
     unsigned best[8];
     int lo[8], len[8], ib0[8];
+    unsigned lb[8];            // kPlaneStageMajor: len and lo + ib0 in one register
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         best[j] = 0xffffffffu;
@@ -617,6 +655,9 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
                 for (int j = 0; j < 8; j++)
                     line_interval(po[j], pa[j], pn[j], high[j] == cm, neg[j], d_out, lo[j],
                                   len[j], ib0[j]);
+#pragma unroll
+                for (int j = 0; j < 8; j++)   // len | first candidate index << 16 (len, index < 4096)
+                    lb[j] = (unsigned)len[j] | ((unsigned)(lo[j] + ib0[j]) << 16);
                 for (int wc = wlo >> 5; wc <= (whi >> 5); wc++) {
                     unsigned m =
                         (unsigned)__builtin_amdgcn_readfirstlane((int)bits[ot * wpo + wc]);
@@ -630,6 +671,38 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
                         unsigned csA[8], csB[8];
                         colsums(RA, reA0, reA1, ob + ca * os, csA);
                         colsums(RB, reB0, reB1, ob + cb * os, csB);
+                        if constexpr (tune::kPlaneStageMajor != 0) {
+                            // the 16 scans stage by stage (independent DPP adds
+                            // between dependent ones: no s_nop), all 8
+                            // ds_bpermute issued before the first is consumed,
+                            // and a branch-free first-minimum update
+                            // rows in groups of G: 2G DPP chains in flight, and
+                            // fewer live registers than all 8 rows at once
+                            constexpr int G = tune::kPlaneStageMajor > 0 ? tune::kPlaneStageMajor : 1;
+#pragma unroll
+                            for (int j0 = 0; j0 < 8; j0 += G) {
+                                unsigned Pa[G], V[G];
+#pragma unroll
+                                for (int j = 0; j < G; j++) { Pa[j] = csA[j0 + j]; V[j] = csB[j0 + j]; }
+                                scan64_dpp_n<G>(Pa, V);
+#pragma unroll
+                                for (int j = 0; j < G; j++) {
+                                    const unsigned ta = (unsigned)__builtin_amdgcn_readlane((int)Pa[j], 63);
+                                    V[j] = lane < W2 - 1 ? V[j] + ta : Pa[j];
+                                    V[j] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)V[j]);
+                                    Pa[j] -= csA[j0 + j];          // exclusive prefix
+                                }
+#pragma unroll
+                                for (int j = 0; j < G; j++) {
+                                    const unsigned sad = V[j] - Pa[j];
+                                    const unsigned tt = (unsigned)(d_in - lo[j0 + j]);
+                                    const unsigned x = lb[j0 + j];
+                                    const unsigned key = (sad << 12) | (tt + (x >> 16));
+                                    const bool on = tt < (x & 0xffffu);
+                                    best[j0 + j] = min(best[j0 + j], on ? key : 0xffffffffu);
+                                }
+                            }
+                        } else {
 #pragma unroll
                         for (int j = 0; j < 8; j++) {
                             const unsigned Pa = scan64_dpp(csA[j]), Pb = scan64_dpp(csB[j]);
@@ -641,6 +714,7 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
                             const unsigned key = (sad << 12) | (unsigned)(d_in + ib0[j]);
                             const bool on = (unsigned)(d_in - lo[j]) < (unsigned)len[j];
                             best[j] = on ? min(best[j], key) : best[j];
+                        }
                         }
                     }
                 }

@@ -200,6 +200,15 @@ constexpr int kCensusCost2Lines = 8;
 constexpr int kPlaneOuKB = 24;      // staged O chunk (KB)
 constexpr int kPlaneWords = 1024;   // offset bitmap per pass: 32K bits
 constexpr int kPlaneMinBlocks = 3;  // __launch_bounds__ min workgroups per CU
+// Plane loop body (round 5): the box-sum scans of G
+// rows at a time stage by stage (2G independent DPP chains: no s_nop), the
+// G ds_bpermute before their uses, a branch-free first-minimum update
+// (kPlaneStageMajor = G in {2, 4, 8}); or row by row (0).
+constexpr int kPlaneStageMajor = 2;
+// line_interval's division by each pixel's a: hoisted by the compiler (0:
+// 32 B/lane of scratch at k = 20, reloaded per outer offset) or recomputed
+// per outer offset (1: no scratch at k = 20, diagonal pairs 9 % slower).
+constexpr int kPlaneNoHoistDiv = 0;
 
 }  // namespace tune
 }  // namespace sva

@@ -201,3 +201,18 @@ def test_gpus_2_without_world_size_gets_past_argument_handling():
     assert r.returncode != 0
     assert "torch.distributed.run" not in r.stderr
     assert "needs a HIP device" in r.stderr or "HIP device(s) visible" in r.stderr
+
+
+def test_batch_groups_and_frames_per_launch(bench):
+    """--batch --streams S: S contiguous batch calls; the roofline's frames per
+    aggregation launch follow sva_disparity_sgm_batch_d's chunks of 8 and
+    sub-batches of 4 (sva_tuning.h kBatchMaxPairs, kBatchSubFrames)."""
+    assert bench.batch_groups(8, 1) == [(0, 8)]
+    assert bench.batch_groups(8, 3) == [(0, 2), (2, 5), (5, 8)]
+    assert bench.batch_groups(2, 3) == [(0, 1), (1, 2), (2, 2)]
+    cover = [j for j0, j1 in bench.batch_groups(11, 4) for j in range(j0, j1)]
+    assert cover == list(range(11))
+    assert bench.batch_frames_per_launch(8) == 4.0           # 8 -> 4 + 4
+    assert bench.batch_frames_per_launch(256) == 4.0
+    assert bench.batch_frames_per_launch(11) == 11 / 3       # 8 -> 4 + 4, 3
+    assert bench.batch_frames_per_launch(8, 3) == 8 / 3      # 2, 3, 3 frames: one launch each
