@@ -156,7 +156,7 @@ def cpu_baseline(W, H, D, threads):
     }
 
 
-def mode_r_beside(ctx, W, H, rows=24, k=20, reps=3):
+def mode_r_beside(ctx, W, H, rows=24, k=20, reps=10):
     """The reference's own path (Mode R: Bresenham candidates + 2k x 2k SAD,
     CameraStereoVision.cpp:44-95), GPU vs its CPU restatement on this host,
     in candidate SADs per second.  Reference rig pair 12 -> 11, k = 20; the
@@ -182,7 +182,8 @@ def mode_r_beside(ctx, W, H, rows=24, k=20, reps=3):
     n_cand = int((np.maximum(np.abs(e[..., 0] - e[..., 2]), np.abs(e[..., 1] - e[..., 3])) + 1)[okn].sum())
     run = lambda: ctx.disparity_ref_d(d_ref.data_ptr(), d_oth.data_ptr(), W, H, W, None, cr, co, k,
                                       0.5, 1.0, d8.data_ptr())
-    run()
+    for _ in range(3):          # warm-up (3 timed reps used to sit in the clock ramp)
+        run()
     torch.cuda.synchronize()
     ctx.set_timing(1)
     ctx.reset_timing()
