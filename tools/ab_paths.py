@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--dir", type=int, default=-1)
+    ap.add_argument("--dir-y", type=int, default=0,
+                    help="2-D array step (census_cost / cost / sgm entries: census_cost2 for "
+                         "supported steps)")
     ap.add_argument("--sub", action="store_true", help="wta_hv / sgm entries: also write the f32 sub-pixel map")
     ap.add_argument("--dmin", type=int, default=0)
     ap.add_argument("--kernels", action="store_true",
@@ -74,7 +77,7 @@ def main():
                                 ct.c_size_t(HCK.numel()), vp(VCK.data_ptr()),
                                 ct.c_size_t(VCK.numel()), W, H, ct.byref(p),
                                 vp(disp.data_ptr()), vp(subm.data_ptr()) if a.sub else None)
-    p = sva.default_params(D=D, dmin=a.dmin, dir=a.dir, subpixel=1 if a.sub else 0)
+    p = sva.default_params(D=D, dmin=a.dmin, dir=a.dir, dir_y=a.dir_y, subpixel=1 if a.sub else 0)
     handles = []
     for path in a.libs:
         lib = ct.CDLL(os.path.abspath(path))
