@@ -100,24 +100,17 @@ const char* sva_status_string(int status);
 /* Pre-size the workspace for W x H x D (optional; calls grow it on demand). */
 int sva_reserve(void* ctx, int width, int height, int D);
 
-/* Path-aggregation route of sva_disparity_sgm* and of the path stage entries
- * (sva_paths_d, sva_paths_tile_d, sva_aggregate_d).  Every route computes the
- * same bytes: census -> W*H*D u8 cost volume -> 8-path kernel writing the four
+/* Path-aggregation route of sva_disparity_sgm*.  COST_VOLUME (= AUTO, the
+ * default): census -> W*H*D u8 cost volume -> 8-path kernel writing the four
  * diagonal volumes and the horizontal / vertical checkpoints -> per-tile
  * recompute of those four directions + WTA (the tile pipeline, DESIGN.md
- * §4.9).  The path kernel has two lane layouts:
- *   AUTO (the default)  one path line per wave for single frames whose
- *                       16-lane launch would not fill the chip (640x480,
- *                       D = 64 / 128 / 256), the 16-lane layout otherwise;
- *   COST_VOLUME         the 16-lane layout (four lines per wave) at every size;
- *   WIDE                one line per wave wherever D is 64, 128 or 256.
- * FUSED (the census-fused path kernel of ABI v1-v3, slower at every D once
- * the checkpoint route existed) was removed in ABI v4: selecting it returns
+ * §4.9).  FUSED (the
+ * census-fused path kernel of ABI v1-v3, slower at every D once the
+ * checkpoint route existed) was removed in ABI v4: selecting it returns
  * SVA_ERR_UNSUPPORTED. */
 #define SVA_PATH_KERNEL_COST_VOLUME 0
 #define SVA_PATH_KERNEL_FUSED 1
 #define SVA_PATH_KERNEL_AUTO 2
-#define SVA_PATH_KERNEL_WIDE 3
 int sva_set_path_kernel(void* ctx, int kernel);
 
 /* Kernel timing with hipEvents on the context stream (measurement only).

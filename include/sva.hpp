@@ -256,8 +256,7 @@ public:
     void check(int s) const {
         if (s != SVA_OK) throw Error(s, sva_last_error(ctx_));
     }
-    // SVA_PATH_KERNEL_AUTO (default), _COST_VOLUME or _WIDE: lane layouts of the
-    // path kernel, the same bytes out (sva.h)
+    // SVA_PATH_KERNEL_AUTO (default) or _COST_VOLUME, the same route (sva.h)
     void setPathKernel(int kernel) { check(sva_set_path_kernel(ctx_, kernel)); }
 
 private:

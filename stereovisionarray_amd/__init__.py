@@ -30,7 +30,6 @@ SVA_ERR_NO_DEVICE = 5
 SVA_PATH_KERNEL_COST_VOLUME = 0
 SVA_PATH_KERNEL_FUSED = 1
 SVA_PATH_KERNEL_AUTO = 2
-SVA_PATH_KERNEL_WIDE = 3
 SVA_TIMING_OFF = 0
 SVA_TIMING_ALL = 1
 SVA_TIMING_PATHS = 2

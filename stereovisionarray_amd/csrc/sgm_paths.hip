@@ -171,13 +171,6 @@ hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, i
     g.ckstr = tg.hck_bytes;
     g.ckvstr = tg.vck_bytes + tg.dck_bytes;
     dim3 grid((unsigned)((2 * g.blk_h + 6 * g.blk_w) * npair));
-    // one line per wave where this launch would leave the SIMDs without
-    // enough waves to hide a step's latency
-    const long long waves = (long long)grid.x * (PATH_BLOCK / 64);
-    if (npair == 1 && paths_wide_supported(D) &&
-        (c.path_layout == SVA_PATH_KERNEL_WIDE ||
-         (c.path_layout == SVA_PATH_KERNEL_AUTO && waves <= tune::kPathsWideMaxWaves)))
-        return launch_paths_wide(c, g, C, L8, CK, CKV);
 #define SVA_PATHS_LAUNCH(DPL_)                                                               \
     hipExtLaunchKernelGGL(sgm_paths_kernel<DPL_>, grid, dim3(PATH_BLOCK), 0, c.stream, t.start, \
                           t.stop, 0, C, L8, CK, CKV, g);                                    \

@@ -601,10 +601,8 @@ int sva_set_path_kernel(void* ctx, int kernel) {
     if (kernel == SVA_PATH_KERNEL_FUSED)
         return fail(c, SVA_ERR_UNSUPPORTED,
                     "the census-fused path kernel was removed in ABI v4 (DESIGN.md §4.5)");
-    if (kernel != SVA_PATH_KERNEL_COST_VOLUME && kernel != SVA_PATH_KERNEL_AUTO &&
-        kernel != SVA_PATH_KERNEL_WIDE)
+    if (kernel != SVA_PATH_KERNEL_COST_VOLUME && kernel != SVA_PATH_KERNEL_AUTO)
         return fail(c, SVA_ERR_INVALID_ARG, "unknown path kernel");
-    c->path_layout = kernel;
     return SVA_OK;
 }
 

@@ -73,9 +73,6 @@ struct Ctx {
     std::vector<hipEvent_t> side_done;
     hipEvent_t fork = nullptr;
     DevBuf census_side;
-    // path-kernel lane layout (sva_set_path_kernel): AUTO picks one line per
-    // wave for frames too small to fill the chip
-    int path_layout = SVA_PATH_KERNEL_AUTO;
 };
 
 // Which launches a timing mode records: SVA_TIMING_ALL every one,
@@ -161,12 +158,6 @@ hipError_t launch_cost(Ctx& c, const uint64_t* cl, const uint64_t* cr, int W, in
 hipError_t launch_paths(Ctx& c, const uint8_t* C, int W, int H, int D, int P1, int P2,
                         uint8_t* L8, uint8_t* CK = nullptr, uint8_t* CKV = nullptr,
                         int npair = 1);
-// sgm_paths_wide.hip: one path line per wave, the same bytes out as
-// launch_paths (single frames; D = 64, 128, 256).  launch_paths calls it.
-namespace sgm { struct PathGeom; }
-bool paths_wide_supported(int D);
-hipError_t launch_paths_wide(Ctx& c, const sgm::PathGeom& g, const uint8_t* C, uint8_t* L8,
-                             uint8_t* CK, uint8_t* CKV);
 // Tile pipeline geometry: tiles of 16 columns x seg rows (seg = 2^seg_log2),
 // checkpoints every seg columns (horizontal lines) and every seg rows
 // (vertical lines).

@@ -35,13 +35,6 @@ constexpr int kCLoadAux = 0;
 // back soon).  nt (2) measured: frame 0.952 vs 0.963 ms median,
 // min 0.948 vs 0.942 -- noise (profiles/r03_v6/ab_retune_sgm.log.txt).
 constexpr int kCkptStoreAux = 0;
-// One path line per wave (sgm_paths_wide.hip) for frames
-// whose 16-lane launch would have at most kPathsWideMaxWaves waves (AUTO
-// route, D = 64 / 128 / 256), and its prefetch ring depth in pixels.
-constexpr int kPathsWideMaxWaves = 2048;
-constexpr int kPfWide = 16;
-// sched_barrier around the wide kernel's ring refill (as in path_line) or none.
-constexpr int kWideSchedBarrier = 0;
 
 // Minimum of a path state restored from a checkpoint (sgm_common.h
 // state_from_words): the packed-u16 min tree of the recurrence step (1) or
