@@ -263,8 +263,6 @@ __device__ __forceinline__ void scan64_dpp_n(unsigned (&a)[N], unsigned (&b)[N])
 //     first-minimum key is the u32 (SAD << 12 | i): SAD < 2^20 for k <= 32,
 //     i < 4096 (Mode R requires W, H < 4096).
 constexpr int P3_ROWS = 32;                          // 4 waves x 8 rows
-constexpr int P3_RW_MAX = 63 + 2 * PT_MAXK;          // region columns
-constexpr int P3_RS = 100;                           // R column stride: 25 dwords (odd)
 constexpr int P3_OU_BYTES = tune::kPlaneOuKB * 1024;  // staged O chunk
 constexpr int P3_WORDS = tune::kPlaneWords;            // offset bitmap per pass: 32K bits
 constexpr int P3_MAX_OUT = 1024;                     // outer offsets per pass
@@ -330,17 +328,29 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     constexpr bool ODD = (W2 & 2) != 0;       // the 2k rows end mid-dword
     constexpr int ND2 = (W2 + 6) / 4 + 1;     // dwords holding rows r0 .. r0 + 2k + 6
     constexpr int RW = 63 + W2;
-    constexpr int RS4 = P3_RS / 4;
-    static_assert(24 + 4 * ND2 <= P3_RS, "R column stride too small");
+    // R column stride: rows r0 + 4*ND2 of the lowest wave, an odd dword count
+    // (each lane reads its own column: conflict-free)
+    constexpr int RS = (((24 + 4 * ND2) / 4) | 1) * 4;
+    constexpr int RS4 = RS / 4;
+    static_assert(24 + 4 * ND2 <= RS, "R column stride too small");
+    // tune::kPlanePoLds: each thread's eight line offsets (po below) in LDS,
+    // [row][thread], read back once per outer offset instead of held in
+    // registers -- where that still leaves kPlaneMinBlocks workgroups per CU
+    constexpr int LDS_BASE = RW * RS + P3_WORDS * 4 + P3_OU_BYTES + 4 * P3_MAX_OUT + 24 +
+                             P3_ROWS * 64 * 2 + 4;
+    constexpr bool POLDS =
+        tune::kPlanePoLds != 0 && LDS_BASE + 8 * 256 * 4 + 256 <= 160 * 1024 / tune::kPlaneMinBlocks;
     static_assert(ND2 >= ND + 2, "entering rows");
+    static_assert(K >= 1 && K <= PT_MAXK, "k outside the ABI range");
     static_assert(4 * K * K * 255 < (1 << 20), "SAD must fit the 20-bit key field");
-    __shared__ __attribute__((aligned(16))) uint8_t RT[P3_RW_MAX * P3_RS];
+    __shared__ __attribute__((aligned(16))) uint8_t RT[RW * RS];
     __shared__ unsigned bits[P3_WORDS];
     __shared__ __attribute__((aligned(16))) uint8_t OUT[P3_OU_BYTES];
     __shared__ short omn[P3_MAX_OUT], omx[P3_MAX_OUT];
     __shared__ int box[6];   // dx_lo, dx_hi, dy_lo, dy_hi, #High pixels, #pixels
     __shared__ unsigned short uniq[P3_ROWS * 64];   // pixels with a distinct relative line
     __shared__ int nuniq;
+    __shared__ int po_lds[POLDS ? 8 * 256 : 1];
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     const int tx0 = K + blockIdx.x * 64, ty0 = K + blockIdx.y * P3_ROWS;
@@ -349,10 +359,10 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     if (t < 6) box[t] = t >= 4 ? 0 : ((t & 1) ? -0x7fffffff : 0x7fffffff);
     // R region, column-major; rows up to the stride are staged as well (read
     // into registers below, masked out of every sum)
-    for (int i = t; i < RW * P3_RS; i += 256) {
+    for (int i = t; i < RW * RS; i += 256) {
         const int v = i / RW, u = i - v * RW;
         const int gx = rx0 + u, gy = ry0 + v;
-        RT[u * P3_RS + v] = (gx < W && gy < H) ? ref[(size_t)gy * pitch + gx] : 0;
+        RT[u * RS + v] = (gx < W && gy < H) ? ref[(size_t)gy * pitch + gx] : 0;
     }
     // this thread's pixels: column tx0 + lane, rows ty0 + r0 + j
     int ox[8], oy[8], pa[8], pn[8];
@@ -539,6 +549,7 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     for (int j = 0; j < 8; j++) {
         const int omaj = high[j] ? oy[j] : ox[j], omin = high[j] ? ox[j] : oy[j];
         po[j] = (omaj & 0xffff) | (omin << 16);
+        if constexpr (POLDS) po_lds[j * 256 + t] = po[j];
     }
     const int in_lo = cm ? dylo : dxlo, out_lo = cm ? dxlo : dylo;
     const int src = ((lane + W2 - 1) & 63) << 2;
@@ -651,6 +662,13 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
                 const int wlo = max(ilo, __builtin_amdgcn_readfirstlane(omn[ot]));
                 const int whi = min(ihi, __builtin_amdgcn_readfirstlane(omx[ot]));
                 if (wlo > whi) continue;
+                if constexpr (POLDS) {
+                    // reload the line offsets here (the empty asm keeps the
+                    // compiler from hoisting the reads out of the loop)
+                    asm volatile("" ::: "memory");
+#pragma unroll
+                    for (int j = 0; j < 8; j++) po[j] = po_lds[j * 256 + t];
+                }
 #pragma unroll
                 for (int j = 0; j < 8; j++)
                     line_interval(po[j], pa[j], pn[j], high[j] == cm, neg[j], d_out, lo[j],

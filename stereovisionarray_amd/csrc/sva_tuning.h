@@ -209,6 +209,10 @@ constexpr int kPlaneStageMajor = 2;
 // 32 B/lane of scratch at k = 20, reloaded per outer offset) or recomputed
 // per outer offset (1: no scratch at k = 20, diagonal pairs 9 % slower).
 constexpr int kPlaneNoHoistDiv = 0;
+// Each thread's eight line offsets in LDS (8 KB per workgroup), reloaded per
+// outer offset, instead of eight VGPRs held across the plane loop (1), at
+// every k whose LDS still leaves kPlaneMinBlocks workgroups per CU.
+constexpr int kPlanePoLds = 1;
 
 }  // namespace tune
 }  // namespace sva
