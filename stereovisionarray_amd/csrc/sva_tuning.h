@@ -24,7 +24,17 @@ namespace tune {
 // 36/12 0.5798 (frames 0.952-0.966 ms, all within noise).  D=64 (1080p) 40/12 0.372 vs 8/8
 // 0.416; D=192 24/8 0.996 vs 12/8 1.154; D=256 (4K) 12/8 (16/8 equal, 20/8
 // and 12/12 +3 %).
-constexpr int kPfH4 = 40, kPfV4 = 12;
+// Round 5, small frames (profiles/r05_v5/prefetch_v/): at 640x480 every
+// direction alone takes 0.054-0.065 ms (direction ablations, abl_*.log.txt)
+// and a vertical line alone pays ~125 ns per step on a 12-step ring, so the
+// vertical / diagonal rings were swept again.  D=64 (kPfV4, sgm_paths ms,
+// two runs each): 12 / 16 / 20 / 24 / 28 / 32 / 40 at 640x480 0.0776 /
+// 0.0757 / 0.0771 / 0.0703 / 0.0793 / 0.0772 / 0.0703, 960x540 all 0.093,
+// 1080p 0.2965 / 0.2895 / 0.2976 / 0.2912 / 0.2978 / 0.2899 / 0.292; 24 is
+// free in registers (the horizontal ring sets the VGPRs).  D=128 (kPfV8) 12 /
+// 16 / 20 / 24 / 32: 640x480 0.1049 / 0.1022 / 0.1031 / 0.1011 / 0.1042 but
+// 1080p 0.5178 / 0.518 / 0.5209 / 0.5261 / 0.5218, so D=128 keeps 12.
+constexpr int kPfH4 = 40, kPfV4 = 24;
 constexpr int kPfH8 = 32, kPfV8 = 12;
 constexpr int kPfH12 = 24, kPfV12 = 8;
 constexpr int kPfH16 = 12, kPfV16 = 8;
