@@ -283,6 +283,25 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
     // those loads land in-range garbage or, past the volume, the buffer range
     // check returns 0 -- never consumed either way.
     Cursor<false> pc = cc;
+    // Checkpoint stores at compile-time step positions (tune::kStaticCkptHits):
+    // with PF a multiple of the segment, step p of every PF-step iteration
+    // sits at the same place in the segment grid once the line is preceded by
+    // `lead` steps (0 for lines that run with x or y, (-W or -H) mod SEG for
+    // the others).  A lead step sees cost 0 from zero state, and zero state
+    // with cost 0 stays zero (u = min(P1, 0, P2) = 0), so the line's first
+    // real pixel still starts from L = C.  The runtime test this replaces put
+    // a taken branch on every step (640x480: horizontal lines alone 0.065 ->
+    // 0.050 ms with static positions, profiles/r05_v5/ckpt_hits/).  Only the
+    // D = 64 kernel takes it (tune::kStaticCkptHitsMaxDpl).
+    constexpr bool STATIC_HITS = DPL <= tune::kStaticCkptHitsMaxDpl && (CKPT == 1 || CKPT == 2) &&
+                                 SL > 0 && PF % (1 << SL) == 0;
+    int lead = 0;
+    if constexpr (STATIC_HITS) {
+        constexpr int SEG = 1 << SL;
+        lead = CKPT == 1 ? (rx > 0 ? 0 : (SEG - W % SEG) % SEG) : (ry > 0 ? 0 : (SEG - H % SEG) % SEG);
+        pc.off -= (unsigned)lead * stride;
+    }
+    const int nsteps = steps + lead;
     // Diagonal lines wrap without per-step x tracking.  Line l visits
     // x = (l + rx*t) mod W and wraps between pixels s and s+1 when s + 1 =
     // W - l (rx = +1) or l + 1 (rx = -1), then every W steps: tw* hold each
@@ -311,6 +330,10 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
 #pragma unroll
     for (int p = 0; p < PF; p++) {
         ring[p] = bload<NW>(rC, pc.off);
+        if constexpr (STATIC_HITS) {   // lead steps: cost 0 (lead < SEG <= PF)
+#pragma unroll
+            for (int w = 0; w < NW; w++) ring[p].w[w] = p < lead ? 0u : ring[p].w[w];
+        }
         pc.off += stride;
         if constexpr (DIAG) {   // the advance past pixel PF-1 is checked by step 0
             if (p < PF - 1) {
@@ -336,7 +359,26 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
         for (int w = 0; w < NW; w++) cw[w] = ring[p].w[w];
         unsigned ow[NW];
         sgm_step<DPL>(cw, A, m, ow, P1, P2, edges);
-        if constexpr (CKPT == 1) {
+        if constexpr (CKPT == 1 && STATIC_HITS) {
+            // the last pixel of a segment (rx > 0) or its first (rx < 0) is at
+            // step p = SEG - 1 of every SEG steps (lead above); not the row's
+            // last / first column
+            constexpr int SEG = 1 << SL;
+            if ((p & (SEG - 1)) == SEG - 1) {
+                const int x = rx > 0 ? ts : W - 1 - (ts - lead);
+                if (rx > 0 ? x + 1 < W : x > 0)
+                    bstore<NW, tune::kCkptStoreAux>(rCK, ((unsigned)(y0 * g.ns + (x >> SL)) * (unsigned)D +
+                                             (unsigned)(k * DPL)), ow);
+            }
+        } else if constexpr (CKPT == 2 && STATIC_HITS) {
+            constexpr int SEG = 1 << SL;
+            if ((p & (SEG - 1)) == SEG - 1) {
+                const int y = ry > 0 ? ts : H - 1 - (ts - lead);
+                if (ry > 0 ? y + 1 < H : y > 0)
+                    bstore<NW, tune::kCkptStoreAux>(rCK, ((unsigned)((y >> SL) * W + x0) * (unsigned)D +
+                                             (unsigned)(k * DPL)), ow);
+            }
+        } else if constexpr (CKPT == 1) {
             // ts is the (wave-uniform) step index; x the pixel just computed
             const int x = rx > 0 ? ts : W - 1 - ts;
             constexpr int SEG = 1 << SL;
@@ -411,14 +453,14 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
     };
 
     int t = 0;
-    for (; t + PF <= steps; t += PF) {
+    for (; t + PF <= nsteps; t += PF) {
 #pragma unroll
         for (int p = 0; p < PF; p++) step(p, true, t + p);
     }
     // tail: fewer than PF steps left, all already in the ring
 #pragma unroll
     for (int p = 0; p < PF; p++)
-        if (t + p < steps) step(p, false, t + p);
+        if (t + p < nsteps) step(p, false, t + p);
 }
 
 

@@ -45,6 +45,16 @@ constexpr int kCLoadAux = 0;
 // back soon).  nt (2) measured: frame 0.952 vs 0.963 ms median,
 // min 0.948 vs 0.942 -- noise (profiles/r03_v6/ab_retune_sgm.log.txt).
 constexpr int kCkptStoreAux = 0;
+// Horizontal / vertical checkpoint stores at compile-time step positions
+// behind 0-7 lead steps, or a runtime segment test every step (sgm_common.h
+// path_line; needs PF a multiple of the segment), for the kernels with at
+// most this many disparities per lane (0: none).  sgm_paths ms, runtime test
+// -> static positions (profiles/r05_v5/ckpt_hits/): 640x480 D=64 0.0703 ->
+// 0.0672, 960x540 D=64 0.0938 -> 0.0821 (frame 0.156 -> 0.145), 1080p D=64
+// 0.2918 -> 0.2889; but 1080p D=128 0.5127 -> 0.5192 and 0.5109 -> 0.5155 in
+// the two variant orders (+0.7 %), D=192 / 4K D=256 within 0.3 %.  So D=64
+// only (DPL 4).
+constexpr int kStaticCkptHitsMaxDpl = 4;
 
 // Minimum of a path state restored from a checkpoint (sgm_common.h
 // state_from_words): the packed-u16 min tree of the recurrence step (1) or
