@@ -177,10 +177,24 @@ __global__ __launch_bounds__(CC_BLOCK) void census_cost_mma_kernel(
 #pragma unroll
             for (int k = 0; k < PXB * NC / CC_BLOCK; k++) {
                 const int ch = t + k * CC_BLOCK;
-                const int lp = ch / NC, ci = ch % NC, x = x0 + lp;
+                int lp, sl;
+                const int ci = ch % NC;
+                if constexpr (tune::kCensusCostSlotOrder) {
+                    // chunks in staging-slot order: the 32 lanes of a read
+                    // group take consecutive slots, whose rows start on
+                    // distinct banks (S4 odd); in pixel order they took
+                    // slots 16 apart, all on one bank set (4-way conflicts)
+                    sl = ch / NC;
+                    const int c = sl / (PXB / 4), r = sl % (PXB / 4), n = r & 15;
+                    lp = 64 * (r >> 4) + 4 * (DIR > 0 ? n : 15 - n) + c;
+                } else {
+                    lp = ch / NC;
+                    const int m = (lp >> 2) & 15, n = DIR > 0 ? m : 15 - m;
+                    sl = (lp & 3) * (PXB / 4) + 16 * (lp >> 6) + n;
+                }
+                const int x = x0 + lp;
                 if (x >= W) continue;
-                const int m = (lp >> 2) & 15, n = DIR > 0 ? m : 15 - m;
-                const unsigned* src = &stg[((lp & 3) * (PXB / 4) + 16 * (lp >> 6) + n) * S4 + 4 * ci];
+                const unsigned* src = &stg[sl * S4 + 4 * ci];
                 unsigned out[4] = {src[0], src[1], src[2], src[3]};
                 if (dreal < D) {                 // padded disparities: cost 255
 #pragma unroll

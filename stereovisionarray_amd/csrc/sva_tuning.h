@@ -212,6 +212,14 @@ constexpr int kCensusCostPx4 = 64, kCensusCostPx8 = 64, kCensusCostPx12 = 64, kC
 // (ab_census_cost_store_threshold.log.txt): 1080p D=128 0.9025 / 0.9215, D=256
 // 1.733 / 1.753, 4K D=256 7.59 / 7.64.
 constexpr int kCostStoreNT = 1;
+// census_cost's store phase reads the staged costs in staging-slot order (1:
+// conflict-free LDS reads at D=128) or in pixel order (0: a read group's 4
+// pixels sit 16 slots apart, all on one bank set, 4-way conflicts; SQ counters
+// at 1080p D=128 had 8.7 M bank-conflict cycles of 30.8 M LDS cycles).
+// census_cost ms 0 -> 1 (profiles/r05_v5/slot_order/): 1080p D=128 0.0951 ->
+// 0.0918, D=192 0.127 -> 0.1247, D=256 0.1418 -> 0.1376, 4K D=256 0.5376 ->
+// 0.5213, D=64 unchanged.
+constexpr int kCensusCostSlotOrder = 1;
 // census_cost2.hip (2-D array steps): adjacent lattice lines per workgroup,
 // which share one staged image patch.
 constexpr int kCensusCost2Lines = 8;
