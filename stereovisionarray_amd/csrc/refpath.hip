@@ -333,13 +333,6 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     constexpr int RS = (((24 + 4 * ND2) / 4) | 1) * 4;
     constexpr int RS4 = RS / 4;
     static_assert(24 + 4 * ND2 <= RS, "R column stride too small");
-    // tune::kPlanePoLds: each thread's eight line offsets (po below) in LDS,
-    // [row][thread], read back once per outer offset instead of held in
-    // registers -- where that still leaves kPlaneMinBlocks workgroups per CU
-    constexpr int LDS_BASE = RW * RS + P3_WORDS * 4 + P3_OU_BYTES + 4 * P3_MAX_OUT + 24 +
-                             P3_ROWS * 64 * 2 + 4;
-    constexpr bool POLDS =
-        tune::kPlanePoLds != 0 && LDS_BASE + 8 * 256 * 4 + 256 <= 160 * 1024 / tune::kPlaneMinBlocks;
     static_assert(ND2 >= ND + 2, "entering rows");
     static_assert(K >= 1 && K <= PT_MAXK, "k outside the ABI range");
     static_assert(4 * K * K * 255 < (1 << 20), "SAD must fit the 20-bit key field");
@@ -350,6 +343,14 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     __shared__ int box[6];   // dx_lo, dx_hi, dy_lo, dy_hi, #High pixels, #pixels
     __shared__ unsigned short uniq[P3_ROWS * 64];   // pixels with a distinct relative line
     __shared__ int nuniq;
+    // tune::kPlanePoLds: each thread's eight line offsets (po below) in LDS,
+    // [row][thread], read back once per outer offset instead of held in
+    // registers -- where that still leaves kPlaneMinBlocks workgroups per CU
+    // (the arrays above plus 256 B of alignment slack)
+    constexpr size_t LDS_BASE = sizeof(RT) + sizeof(bits) + sizeof(OUT) + sizeof(omn) + sizeof(omx) +
+                                sizeof(box) + sizeof(uniq) + sizeof(nuniq);
+    constexpr bool POLDS = tune::kPlanePoLds != 0 &&
+                           LDS_BASE + 8 * 256 * sizeof(int) + 256 <= 160 * 1024 / tune::kPlaneMinBlocks;
     __shared__ int po_lds[POLDS ? 8 * 256 : 1];
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
