@@ -140,7 +140,8 @@ __device__ __forceinline__ void match_pixel_wave(const uint8_t* __restrict__ ref
                                                  size_t pitch, int x, int y, const int4 e, int k,
                                                  uint8_t* __restrict__ disp_u8,
                                                  uint16_t* __restrict__ disp_u16,
-                                                 uint8_t* __restrict__ valid_out) {
+                                                 uint8_t* __restrict__ valid_out,
+                                                 unsigned* __restrict__ keys = nullptr) {
     const int lane = threadIdx.x & 63;
     const size_t p = (size_t)y * W + x;
     const Line L = make_line(e.x, e.y, e.z, e.w);                     // :73
@@ -164,7 +165,11 @@ __device__ __forceinline__ void match_pixel_wave(const uint8_t* __restrict__ ref
         key = wave_min_u64(key);                                      // :85 first min
         best = key < best ? key : best;
     }
-    if (lane == 0) {
+    if (lane == 0 && keys) {
+        // the split plane loop's first-minimum key (SAD << 12 | i), finished
+        // by ref_finalize_kernel
+        atomicMin(&keys[p], ((unsigned)(best >> 32) << 12) | (unsigned)(best & 0xfffu));
+    } else if (lane == 0) {
         int cx, cy;
         line_point(L, (int)(best & 0xffffffffu), cx, cy);
         const double dx = (double)(cx - x), dy = (double)(cy - y);
@@ -322,7 +327,13 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     const uint8_t* __restrict__ ref, const uint8_t* __restrict__ other, int W, int H, size_t pitch,
     const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
     const uint8_t* __restrict__ valid_in, uint8_t* __restrict__ disp_u8,
-    uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out) {
+    uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out,
+    unsigned* __restrict__ keys) {
+    // keys != nullptr: the tile's inner offsets are split over gridDim.z
+    // workgroups (blockIdx.z = this one's share), and each pixel's first-
+    // minimum key goes to keys[] by atomicMin (ref_finalize_kernel turns it
+    // into the disparity).  The key order is the reference's first minimum
+    // whatever the split (CameraStereoVision.cpp:85).
     constexpr int W2 = 2 * K;
     constexpr int ND = (W2 + 3) / 4;          // dwords holding a 2k-row column
     constexpr bool ODD = (W2 & 2) != 0;       // the 2k rows end mid-dword
@@ -437,13 +448,14 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     if (opp < 1 || stage_bytes(1, 1) > P3_OU_BYTES) {
         // one outer offset's bitmap row or O column does not fit: per-pixel
         // waves for this tile
+        if (blockIdx.z != 0) return;      // one share does the whole tile
         for (int pi = wv; pi < 64 * P3_ROWS; pi += 4) {
             const int x = tx0 + (pi & 63), y = ty0 + (pi >> 6);
             if (x >= W - K || y >= H - K) continue;
             const size_t p = (size_t)y * W + x;
             if (!valid_in[p] || (mask && mask[p] == 0)) continue;
             match_pixel_wave<ND>(ref, other, W, pitch, x, y, ends[p], K, disp_u8, disp_u16,
-                                 valid_out);
+                                 valid_out, keys);
         }
         return;
     }
@@ -555,8 +567,24 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     const int in_lo = cm ? dylo : dxlo, out_lo = cm ? dxlo : dylo;
     const int src = ((lane + W2 - 1) & 63) << 2;
     const int bstride = wpo * 32;
-    for (int oa = 0; oa < n_out; oa += opp) {
-        const int nl = min(n_out - oa, opp);    // outer offsets of this bitmap pass
+    // this workgroup's share of the INNER offsets (all of them unsplit): the
+    // runs along the inner axis are the long ones, so every share gets a
+    // piece of every outer offset's run -- an outer-offset split left the
+    // thin bands of Low / High pairs with one or two uneven outer offsets
+    // per share
+    // (tune::kPlaneSplitInner: 1 inner, 0 outer, 2 per tile -- inner for the
+    // thin offset bands of Low / High pairs, outer for the diagonal bands,
+    // whose inner runs are short and shift with the outer offset)
+    const bool SPLIT_IN = tune::kPlaneSplitInner == 2 ? 4 * min(bw, bh) < max(bw, bh)
+                                                       : tune::kPlaneSplitInner != 0;
+    const int nsplit = SPLIT_IN ? n_in : n_out;
+    const int s_lo = (int)((long long)nsplit * blockIdx.z / gridDim.z);
+    const int s_hi = (int)((long long)nsplit * (blockIdx.z + 1) / gridDim.z);
+    const int i_lo = SPLIT_IN ? s_lo : 0;
+    const unsigned i_len = (unsigned)(SPLIT_IN ? s_hi - s_lo : n_in);
+    const int o_lo = SPLIT_IN ? 0 : s_lo, o_hi = SPLIT_IN ? n_out : s_hi;
+    for (int oa = o_lo; oa < o_hi; oa += opp) {
+        const int nl = min(o_hi - oa, opp);     // outer offsets of this bitmap pass
         __syncthreads();                     // the previous pass's planes are done
         for (int i = t; i < wpo * nl; i += 256) bits[i] = 0;
         __syncthreads();
@@ -578,7 +606,7 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
                 const int rx = L.high ? bx0 + off : bx0 + i;
                 const int ry = L.high ? by0 + i : by0 + off;
                 const int ro = (cm ? rx : ry) - oa;
-                if ((unsigned)ro < (unsigned)nl) {
+                if ((unsigned)ro < (unsigned)nl && (unsigned)((cm ? ry : rx) - i_lo) < i_len) {
                     const int b = ro * bstride + (cm ? ry : rx);
                     if ((b >> 5) != cur) {
                         if (msk) atomicOr(&bits[cur], msk);
@@ -741,6 +769,14 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
             if (wst < 0) o0 = o1;
         }
     }
+    if (keys) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if ((pn[j] & 0xffff) == 0 || best[j] == 0xffffffffu) continue;
+            atomicMin(&keys[(size_t)(ty0 + r0 + j) * W + tx0 + lane], best[j]);
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         if ((pn[j] & 0xffff) == 0) continue;
@@ -755,6 +791,28 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
         if (disp_u16) disp_u16[p] = (uint16_t)dn;
         if (valid_out) valid_out[p] = 1;
     }
+}
+
+// The split plane loop's keys -> the reference's outputs: candidate i of the
+// pixel's line, (uchar)(int)sqrt(dx^2 + dy^2) (CameraStereoVision.cpp:85-89).
+// Pixels without a key (not matched) keep what the maps held.
+__global__ void ref_finalize_kernel(int W, int H, const int4* __restrict__ ends,
+                                    const unsigned* __restrict__ keys,
+                                    uint8_t* __restrict__ disp_u8, uint16_t* __restrict__ disp_u16,
+                                    uint8_t* __restrict__ valid_out) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= W) return;
+    const size_t p = (size_t)y * W + x;
+    const unsigned key = keys[p];
+    if (key == 0xffffffffu) return;
+    const int4 e = ends[p];
+    int cx, cy;
+    line_point(make_line(e.x, e.y, e.z, e.w), (int)(key & 0xfffu), cx, cy);
+    const double dx = (double)(cx - x), dy = (double)(cy - y);
+    const int dn = (int)__builtin_sqrt(dx * dx + dy * dy);       // :89
+    disp_u8[p] = (uint8_t)dn;
+    if (disp_u16) disp_u16[p] = (uint16_t)dn;
+    if (valid_out) valid_out[p] = 1;
 }
 
 __global__ void disp_to_depth_kernel(const uint8_t* __restrict__ disp, int n, double num,
@@ -777,6 +835,23 @@ hipError_t launch_ref_endpoints(Ctx& c, int W, int H, const sva_camera& cref,
     return hipGetLastError();
 }
 
+// Workgroups per tile for the plane kernel: the tile grid is split over the
+// outer offsets when that fills the chip's workgroup slots better.  Modelled
+// time ~ rounds(tiles * S / slots) * (1 / S + kPlaneSplitOverhead); S = 1 (the
+// unsplit kernel writing its outputs directly) when that is best.
+static int plane_split(long long tiles, int cu_count) {
+    if (tune::kPlaneSplitMax <= 1) return 1;
+    const long long slots = (long long)cu_count * tune::kPlaneMinBlocks;
+    int best = 1;
+    double tbest = 1e30;
+    for (int S = 1; S <= tune::kPlaneSplitMax; S++) {
+        const double rounds = (double)((tiles * S + slots - 1) / slots);
+        const double t = rounds * (1.0 / S + (S > 1 ? tune::kPlaneSplitOverhead : 0.0));
+        if (t < tbest - 1e-9) { tbest = t; best = S; }
+    }
+    return best;
+}
+
 hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, int W, int H,
                             size_t pitch, const uint8_t* mask, const int32_t* ends,
                             const uint8_t* valid_in, int k, uint8_t* disp_u8,
@@ -785,13 +860,28 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
     const long long npx = (long long)(W - 2 * k) * (H - 2 * k);
     if (npx <= 0) return hipSuccess;
     // offset-plane algorithm for every k (sva_api checks 1 <= k <= 32)
-    const dim3 pg3((unsigned)((W - 2 * k + 63) / 64),
-                   (unsigned)((H - 2 * k + P3_ROWS - 1) / P3_ROWS));
+    const unsigned gx = (unsigned)((W - 2 * k + 63) / 64), gy = (unsigned)((H - 2 * k + P3_ROWS - 1) / P3_ROWS);
+    int S = plane_split((long long)gx * gy, c.cu_count);
+    // test hook: SVA_PLANE_SPLIT=n forces n shares per tile (1..16), so the
+    // parity tests cover the split route at every size
+    if (const char* e = std::getenv("SVA_PLANE_SPLIT")) {
+        const int n = std::atoi(e);
+        if (n >= 1 && n <= 16) S = n;
+    }
+    unsigned* keys = nullptr;
+    if (S > 1) {
+        hipError_t e = c.ref_keys.ensure((size_t)W * H * sizeof(unsigned));
+        if (e != hipSuccess) return e;
+        keys = (unsigned*)c.ref_keys.ptr;
+        e = hipMemsetAsync(keys, 0xff, (size_t)W * H * sizeof(unsigned), c.stream);
+        if (e != hipSuccess) return e;
+    }
+    const dim3 pg3(gx, gy, (unsigned)S);
 #define SVA_PLANE3_CASE(K_)                                                                    \
     case K_:                                                                                   \
         hipLaunchKernelGGL(ref_plane3_kernel<K_>, pg3, dim3(256), 0, c.stream, ref, other, W, H, \
                            pitch, mask, (const int4*)ends, valid_in, disp_u8, disp_u16,         \
-                           valid_out);                                                         \
+                           valid_out, keys);                                                   \
         break;
     switch (k) {
         SVA_PLANE3_CASE(1) SVA_PLANE3_CASE(2) SVA_PLANE3_CASE(3) SVA_PLANE3_CASE(4)
@@ -805,6 +895,10 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
         default: return hipErrorInvalidValue;
     }
 #undef SVA_PLANE3_CASE
+    if (S > 1)
+        hipLaunchKernelGGL(ref_finalize_kernel, dim3((unsigned)((W + 255) / 256), (unsigned)H),
+                           dim3(256), 0, c.stream, W, H, (const int4*)ends, keys, disp_u8,
+                           disp_u16, valid_out);
     return hipGetLastError();
 }
 

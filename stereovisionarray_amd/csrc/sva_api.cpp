@@ -552,7 +552,7 @@ int sva_destroy(void* ctx) {
     c->census_side.release();
     for (DevBuf* b : {&c->census_l, &c->census_r, &c->cost, &c->paths, &c->ckpt, &c->scratch_u16,
                       &c->disp_r, &c->in_a, &c->in_b, &c->in_mask, &c->out_a, &c->out_b,
-                      &c->out_c, &c->in_c, &c->shifted, &c->keys, &c->counts, &c->total})
+                      &c->out_c, &c->in_c, &c->shifted, &c->keys, &c->counts, &c->total, &c->ref_keys})
         b->release();
     c->timer.release_all();
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);

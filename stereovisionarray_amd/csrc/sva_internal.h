@@ -63,6 +63,8 @@ struct Ctx {
     DevBuf in_a, in_b, in_mask, out_a, out_b, out_c;
     // refinement / 3-D workspace (refine.hip)
     DevBuf in_c, shifted, keys, counts, total;
+    // Mode R's split plane loop: one first-minimum key per pixel (refpath.hip)
+    DevBuf ref_keys;
     int cu_count = 256;
     // sva_batch_sgm's per-context pipeline (copy streams, events, pinned and
     // device staging), created on first use and kept for later calls

@@ -258,3 +258,64 @@ def test_ref_path_4k_row_sampled(ctx, sva, oracle, pair):
     assert np.array_equal(valid, ov)
     assert np.array_equal(d16, o16)
     assert np.array_equal(d8, o8)
+
+
+# The split plane loop (refpath.hip: a tile's inner offsets over several
+# workgroups, first-minimum keys meeting by atomicMin, ref_finalize_kernel):
+# the host picks it for tile grids that fill the chip poorly (the reference's
+# half-size frames); SVA_PLANE_SPLIT forces a share count so that every size
+# and the per-pixel fallback run through it too.
+@pytest.fixture()
+def plane_split(monkeypatch):
+    def set_(n):
+        monkeypatch.setenv("SVA_PLANE_SPLIT", str(n))
+    return set_
+
+
+@pytest.mark.parametrize("shares", [1, 2, 3, 7])
+@pytest.mark.parametrize("pair", [(12, 11), (12, 7), (12, 6), (12, 18)])
+def test_ref_path_split_shares_vga(ctx, sva, oracle, plane_split, shares, pair):
+    W, H, k = 640, 480, 20
+    plane_split(shares)
+    cr, co, ocr, oco = cams_for(sva, oracle, W, *pair)
+    a = synth.texture(H, W, 7 + pair[1])
+    gx, gy = pair[1] % 5 - 2, pair[1] // 5 - 2
+    b = np.roll(np.roll(a, -60 * gy, axis=0), -60 * gx, axis=1)
+    # the maps start non-zero: pixels no share matches keep their value
+    d8_0 = np.full((H, W), 201, np.uint8)
+    d16_0 = np.full((H, W), 40000, np.uint16)
+    v_0 = np.zeros((H, W), np.uint8)
+    mask = np.ones((H, W), np.uint8)
+    mask[200:260, 300:380] = 0
+    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k, mask=mask, disp_u8=d8_0.copy(),
+                                       disp_u16=d16_0.copy(), valid=v_0.copy())
+    o8, o16, ov, _ = oracle.ref_pair(a, b, ocr, oco, k=k, mask=mask, disp_u8=d8_0.copy(),
+                                     disp_u16=d16_0.copy(), valid=v_0.copy())
+    assert ov.sum() > 0
+    assert np.array_equal(valid, ov) and np.array_equal(d16, o16) and np.array_equal(d8, o8)
+
+
+@pytest.mark.parametrize("shares", [2, 5])
+def test_ref_path_split_fallback_diagonal_jump(ctx, sva, oracle, plane_split, shares):
+    """The per-pixel fallback tiles of test_ref_path_plane_fallback_diagonal_jump
+    through the split route: share 0 matches them and leaves keys too."""
+    plane_split(shares)
+    W, H, k = 1920, 1080, 20
+    grid = synth.reference_array(0.036 / W)
+    cr, co = sva.Camera.make(*grid[12]), sva.Camera.make(*grid[0])
+    ocr, oco = oracle.OCamera.make(*grid[12]), oracle.OCamera.make(*grid[0])
+    a = synth.texture(H, W, 8)
+    b = np.roll(np.roll(a, 400, axis=0), 400, axis=1)
+    mask = np.zeros((H, W), np.uint8)
+    mask[100:104, 300:500] = 1
+    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k, mask=mask)
+    o8, o16, ov, n = oracle.ref_pair(a, b, ocr, oco, k=k, mask=mask)
+    assert n > 0 and ov.sum() > 0
+    assert np.array_equal(valid, ov) and np.array_equal(d16, o16) and np.array_equal(d8, o8)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("pair", [(12, 11), (12, 6)])
+def test_ref_path_split_1080p_row_sampled(ctx, sva, oracle, plane_split, pair):
+    plane_split(3)
+    test_ref_path_1080p_row_sampled(ctx, sva, oracle, pair)
