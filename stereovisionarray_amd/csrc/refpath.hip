@@ -328,12 +328,13 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
     const uint8_t* __restrict__ valid_in, uint8_t* __restrict__ disp_u8,
     uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out,
-    unsigned* __restrict__ keys) {
-    // keys != nullptr: the tile's inner offsets are split over gridDim.z
-    // workgroups (blockIdx.z = this one's share), and each pixel's first-
-    // minimum key goes to keys[] by atomicMin (ref_finalize_kernel turns it
-    // into the disparity).  The key order is the reference's first minimum
-    // whatever the split (CameraStereoVision.cpp:85).
+    unsigned* __restrict__ keys, int gx, int t1, int nsh) {
+    // Tiles (gx per row) in dispatch order: blocks [0, t1) are tiles 0 .. t1-1
+    // whole, and every later tile is split over nsh workgroups (one share of
+    // its offsets each) whose per-pixel first-minimum keys meet in keys[] by
+    // atomicMin (ref_finalize_kernel turns them into the disparity).  The key
+    // order is the reference's first minimum whatever the split
+    // (CameraStereoVision.cpp:85).  t1 = all tiles: no split at all.
     constexpr int W2 = 2 * K;
     constexpr int ND = (W2 + 3) / 4;          // dwords holding a 2k-row column
     constexpr bool ODD = (W2 & 2) != 0;       // the 2k rows end mid-dword
@@ -365,7 +366,24 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     __shared__ int po_lds[POLDS ? 8 * 256 : 1];
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int tx0 = K + blockIdx.x * 64, ty0 = K + blockIdx.y * P3_ROWS;
+    // the split tiles are a band in the middle of the frame (tune::
+    // kPlaneSplitMiddle; else the last ones): border tiles carry less work
+    // where a pair's endpoints leave the image, which made a bottom band of
+    // split tiles a poor sample of the frame
+    int tile, share = 0, nshare = 1;
+    const int ntiles = gx * (int)((H - 2 * K + P3_ROWS - 1) / P3_ROWS);
+    const int m0 = tune::kPlaneSplitMiddle ? t1 / 2 : t1;     // first split tile
+    const int nsp = ntiles - t1;                               // split tiles
+    if ((int)blockIdx.x < t1) {
+        tile = (int)blockIdx.x < m0 ? (int)blockIdx.x : (int)blockIdx.x + nsp;
+    } else {
+        const int b = (int)blockIdx.x - t1;
+        tile = m0 + b / nsh;
+        share = b - (tile - m0) * nsh;
+        nshare = nsh;
+    }
+    if (nshare == 1) keys = nullptr;     // a whole tile writes its pixels directly
+    const int tx0 = K + (tile % gx) * 64, ty0 = K + (tile / gx) * P3_ROWS;
     const int rx0 = tx0 - K, ry0 = ty0 - K;   // region origin (image coords)
     const int r0 = 8 * wv;
     if (t < 6) box[t] = t >= 4 ? 0 : ((t & 1) ? -0x7fffffff : 0x7fffffff);
@@ -448,7 +466,7 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     if (opp < 1 || stage_bytes(1, 1) > P3_OU_BYTES) {
         // one outer offset's bitmap row or O column does not fit: per-pixel
         // waves for this tile
-        if (blockIdx.z != 0) return;      // one share does the whole tile
+        if (share != 0) return;           // one share does the whole tile
         for (int pi = wv; pi < 64 * P3_ROWS; pi += 4) {
             const int x = tx0 + (pi & 63), y = ty0 + (pi >> 6);
             if (x >= W - K || y >= H - K) continue;
@@ -578,8 +596,8 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     const bool SPLIT_IN = tune::kPlaneSplitInner == 2 ? 4 * min(bw, bh) < max(bw, bh)
                                                        : tune::kPlaneSplitInner != 0;
     const int nsplit = SPLIT_IN ? n_in : n_out;
-    const int s_lo = (int)((long long)nsplit * blockIdx.z / gridDim.z);
-    const int s_hi = (int)((long long)nsplit * (blockIdx.z + 1) / gridDim.z);
+    const int s_lo = (int)((long long)nsplit * share / nshare);
+    const int s_hi = (int)((long long)nsplit * (share + 1) / nshare);
     const int i_lo = SPLIT_IN ? s_lo : 0;
     const unsigned i_len = (unsigned)(SPLIT_IN ? s_hi - s_lo : n_in);
     const int o_lo = SPLIT_IN ? 0 : s_lo, o_hi = SPLIT_IN ? n_out : s_hi;
@@ -835,21 +853,28 @@ hipError_t launch_ref_endpoints(Ctx& c, int W, int H, const sva_camera& cref,
     return hipGetLastError();
 }
 
-// Workgroups per tile for the plane kernel: the tile grid is split over the
-// outer offsets when that fills the chip's workgroup slots better.  Modelled
-// time ~ rounds(tiles * S / slots) * (1 / S + kPlaneSplitOverhead); S = 1 (the
-// unsplit kernel writing its outputs directly) when that is best.
-static int plane_split(long long tiles, int cu_count) {
-    if (tune::kPlaneSplitMax <= 1) return 1;
+// The plane kernel's tiles and workgroups: whole tiles fill as many full
+// rounds of the chip's workgroup slots as they can, and the tiles left over
+// for a last, partial round are split into the most shares (up to
+// kPlaneSplitMax) that still fit one round -- so the last round ends with
+// short shares instead of a few whole tiles on an idle chip.  Frames with
+// fewer tiles than slots (640x480: 140 tiles for 768 slots) split them all.
+struct PlaneGrid {
+    int t1;     // whole tiles
+    int nsh;    // shares per later tile (1: no split)
+};
+static PlaneGrid plane_grid(long long tiles, int cu_count) {
     const long long slots = (long long)cu_count * tune::kPlaneMinBlocks;
-    int best = 1;
-    double tbest = 1e30;
-    for (int S = 1; S <= tune::kPlaneSplitMax; S++) {
-        const double rounds = (double)((tiles * S + slots - 1) / slots);
-        const double t = rounds * (1.0 / S + (S > 1 ? tune::kPlaneSplitOverhead : 0.0));
-        if (t < tbest - 1e-9) { tbest = t; best = S; }
-    }
-    return best;
+    PlaneGrid g{(int)tiles, 1};
+    if (tune::kPlaneSplitMax <= 1 || slots <= 0) return g;
+    const long long t1 = tiles / slots * slots, rest = tiles - t1;
+    if (rest == 0) return g;
+    long long s = slots / rest;
+    if (s > tune::kPlaneSplitMax) s = tune::kPlaneSplitMax;
+    if (s < 2) return g;
+    g.t1 = (int)t1;
+    g.nsh = (int)s;
+    return g;
 }
 
 hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, int W, int H,
@@ -860,28 +885,31 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
     const long long npx = (long long)(W - 2 * k) * (H - 2 * k);
     if (npx <= 0) return hipSuccess;
     // offset-plane algorithm for every k (sva_api checks 1 <= k <= 32)
-    const unsigned gx = (unsigned)((W - 2 * k + 63) / 64), gy = (unsigned)((H - 2 * k + P3_ROWS - 1) / P3_ROWS);
-    int S = plane_split((long long)gx * gy, c.cu_count);
-    // test hook: SVA_PLANE_SPLIT=n forces n shares per tile (1..16), so the
-    // parity tests cover the split route at every size
+    const int gx = (W - 2 * k + 63) / 64, gy = (H - 2 * k + P3_ROWS - 1) / P3_ROWS;
+    const long long tiles = (long long)gx * gy;
+    PlaneGrid pg = plane_grid(tiles, c.cu_count);
+    // test hook: SVA_PLANE_SPLIT=n splits every tile into n shares (1..16),
+    // so the parity tests cover the split route at every size
     if (const char* e = std::getenv("SVA_PLANE_SPLIT")) {
         const int n = std::atoi(e);
-        if (n >= 1 && n <= 16) S = n;
+        if (n >= 1 && n <= 16) pg = n > 1 ? PlaneGrid{0, n} : PlaneGrid{(int)tiles, 1};
     }
+    const bool split = pg.nsh > 1 && pg.t1 < tiles;
+    const long long nblk = pg.t1 + (tiles - pg.t1) * (split ? pg.nsh : 1);
     unsigned* keys = nullptr;
-    if (S > 1) {
+    if (split) {
         hipError_t e = c.ref_keys.ensure((size_t)W * H * sizeof(unsigned));
         if (e != hipSuccess) return e;
         keys = (unsigned*)c.ref_keys.ptr;
         e = hipMemsetAsync(keys, 0xff, (size_t)W * H * sizeof(unsigned), c.stream);
         if (e != hipSuccess) return e;
     }
-    const dim3 pg3(gx, gy, (unsigned)S);
+    const dim3 pg3((unsigned)nblk);
 #define SVA_PLANE3_CASE(K_)                                                                    \
     case K_:                                                                                   \
         hipLaunchKernelGGL(ref_plane3_kernel<K_>, pg3, dim3(256), 0, c.stream, ref, other, W, H, \
                            pitch, mask, (const int4*)ends, valid_in, disp_u8, disp_u16,         \
-                           valid_out, keys);                                                   \
+                           valid_out, keys, gx, pg.t1, pg.nsh);                                \
         break;
     switch (k) {
         SVA_PLANE3_CASE(1) SVA_PLANE3_CASE(2) SVA_PLANE3_CASE(3) SVA_PLANE3_CASE(4)
@@ -895,7 +923,7 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
         default: return hipErrorInvalidValue;
     }
 #undef SVA_PLANE3_CASE
-    if (S > 1)
+    if (split)
         hipLaunchKernelGGL(ref_finalize_kernel, dim3((unsigned)((W + 255) / 256), (unsigned)H),
                            dim3(256), 0, c.stream, W, H, (const int4*)ends, keys, disp_u8,
                            disp_u16, valid_out);

@@ -241,23 +241,22 @@ constexpr int kPlaneNoHoistDiv = 0;
 // outer offset, instead of eight VGPRs held across the plane loop (1), at
 // every k whose LDS still leaves kPlaneMinBlocks workgroups per CU.
 constexpr int kPlanePoLds = 1;
-// Split each tile's offsets over up to kPlaneSplitMax workgroups when the
-// tile grid fills the chip's workgroup slots poorly; the per-pixel keys then
-// meet in global memory by atomicMin (refpath.hip, ref_finalize_kernel).
-// kPlaneSplitOverhead: a share's fixed cost (R staging, line setup, the
-// bitmap walk over every distinct line) as a fraction of a whole tile's time,
-// in the host's model rounds(tiles * S / slots) * (1 / S + overhead).
-// kPlaneSplitInner: shares of the inner offsets (1), of the outer offsets
-// (0), or per tile by its offset box (2).  ref_match ms, in-process, unsplit
-// / inner / outer (profiles/r05_v5/plane_split/): 960x540 12->11 0.216 /
-// 0.157 / 0.178, 12->7 0.209 / 0.153 / 0.177, 12->6 0.298 / 0.194 / 0.185,
-// 12->18 0.278 / 0.185 / 0.176; 640x480 12->11 0.147 / 0.091 / 0.104, 12->6
-// 0.205 / 0.106 / 0.098.  At 1080p (990 tiles, 1.3 rounds) splitting gave
-// -9 % (12->11) to +4 % (12->7) and at 1280x720 +3 %: overhead 0.25 keeps
-// both unsplit.
+// The tiles left over for the plane kernel's last, partial round of
+// workgroup slots (all of them when a frame has fewer tiles than slots) are
+// split into up to kPlaneSplitMax shares of their offsets, each its own
+// workgroup; the per-pixel keys meet in global memory by atomicMin
+// (refpath.hip plane_grid, ref_finalize_kernel).  kPlaneSplitInner: shares
+// of the inner offsets (1), of the outer offsets (0), or per tile by its
+// offset box (2).  ref_match ms, in-process, unsplit / inner / outer, every
+// tile split (profiles/r05_v5/plane_split/): 960x540 12->11 0.216 / 0.157 /
+// 0.178, 12->7 0.209 / 0.153 / 0.177, 12->6 0.298 / 0.194 / 0.185, 12->18
+// 0.278 / 0.185 / 0.176; 640x480 12->11 0.147 / 0.091 / 0.104, 12->6 0.205 /
+// 0.106 / 0.098; at 1080p every tile split gave -9 % (12->11) to +4 %
+// (12->7), the reason only the last round's tiles are split there.
 constexpr int kPlaneSplitMax = 6;
-constexpr double kPlaneSplitOverhead = 0.25;
 constexpr int kPlaneSplitInner = 2;
+// The split tiles: a band in the middle of the frame (1) or the last tiles (0).
+constexpr int kPlaneSplitMiddle = 1;
 
 }  // namespace tune
 }  // namespace sva
