@@ -328,13 +328,13 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
     const uint8_t* __restrict__ valid_in, uint8_t* __restrict__ disp_u8,
     uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out,
-    unsigned* __restrict__ keys, int gx, int t1, int nsh) {
-    // Tiles (gx per row) in dispatch order: blocks [0, t1) are tiles 0 .. t1-1
-    // whole, and every later tile is split over nsh workgroups (one share of
-    // its offsets each) whose per-pixel first-minimum keys meet in keys[] by
-    // atomicMin (ref_finalize_kernel turns them into the disparity).  The key
-    // order is the reference's first minimum whatever the split
-    // (CameraStereoVision.cpp:85).  t1 = all tiles: no split at all.
+    unsigned* __restrict__ keys) {
+    // Grid (shares, tiles x, tiles y): every tile is split over gridDim.x
+    // workgroups (one share of its offsets each, adjacent in dispatch order)
+    // whose per-pixel first-minimum keys meet in keys[] by atomicMin
+    // (ref_finalize_kernel turns them into the disparity).  The key order is
+    // the reference's first minimum whatever the split
+    // (CameraStereoVision.cpp:85).  gridDim.x = 1: no split, no keys.
     constexpr int W2 = 2 * K;
     constexpr int ND = (W2 + 3) / 4;          // dwords holding a 2k-row column
     constexpr bool ODD = (W2 & 2) != 0;       // the 2k rows end mid-dword
@@ -366,24 +366,11 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     __shared__ int po_lds[POLDS ? 8 * 256 : 1];
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-    // the split tiles are a band in the middle of the frame (tune::
-    // kPlaneSplitMiddle; else the last ones): border tiles carry less work
-    // where a pair's endpoints leave the image, which made a bottom band of
-    // split tiles a poor sample of the frame
-    int tile, share = 0, nshare = 1;
-    const int ntiles = gx * (int)((H - 2 * K + P3_ROWS - 1) / P3_ROWS);
-    const int m0 = tune::kPlaneSplitMiddle ? t1 / 2 : t1;     // first split tile
-    const int nsp = ntiles - t1;                               // split tiles
-    if ((int)blockIdx.x < t1) {
-        tile = (int)blockIdx.x < m0 ? (int)blockIdx.x : (int)blockIdx.x + nsp;
-    } else {
-        const int b = (int)blockIdx.x - t1;
-        tile = m0 + b / nsh;
-        share = b - (tile - m0) * nsh;
-        nshare = nsh;
-    }
+    // (a share taken from a per-tile condition instead -- whole tiles plus a
+    // split band -- cost 4-5 VGPRs and 20 B of scratch at k = 20)
+    const int share = (int)blockIdx.x, nshare = (int)gridDim.x;
     if (nshare == 1) keys = nullptr;     // a whole tile writes its pixels directly
-    const int tx0 = K + (tile % gx) * 64, ty0 = K + (tile / gx) * P3_ROWS;
+    const int tx0 = K + (int)blockIdx.y * 64, ty0 = K + (int)blockIdx.z * P3_ROWS;
     const int rx0 = tx0 - K, ry0 = ty0 - K;   // region origin (image coords)
     const int r0 = 8 * wv;
     if (t < 6) box[t] = t >= 4 ? 0 : ((t & 1) ? -0x7fffffff : 0x7fffffff);
@@ -614,12 +601,28 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
             const int pl = uniq[q], x = tx0 + (pl & 63), y = ty0 + (pl >> 6);
             const int4 e = ends[(size_t)y * W + x];
             const Line L = make_line(e.x, e.y, e.z, e.w);
-            int mnr = L.b > 0 ? (L.major - 1) / L.b : 0;
-            int rem = L.b > 0 ? (L.major - 1) - mnr * L.b : 0;
             const int bx0 = L.x0 - x - dxlo, by0 = L.y0 - y - dylo;
+            // only the points whose major-axis coordinate (b0 + i) can lie in
+            // this pass's outer range or this share's inner range, whichever
+            // axis is the line's major one: a share or a later pass no longer
+            // re-walks the whole line (tune::kPlaneWalkRange)
+            int i0 = 0, i1 = L.n;
+            if constexpr (tune::kPlaneWalkRange != 0) {
+                const bool outer_major = cm != (L.high != 0);   // outer axis x (cm) is Low's major
+                const int b0 = L.high ? by0 : bx0;
+                const int lo = outer_major ? oa : i_lo;
+                const int len = outer_major ? nl : (int)i_len;
+                i0 = max(0, lo - b0);
+                i1 = min(L.n, lo + len - b0);
+            }
+            // minor offset of point i: floor((a i + major - 1) / b), then
+            // advanced incrementally (it grows by at most one per step, a <= b)
+            const int num0 = L.a * i0 + L.major - 1;
+            int mnr = L.b > 0 ? num0 / L.b : 0;
+            int rem = L.b > 0 ? num0 - mnr * L.b : 0;
             int cur = -1;
             unsigned msk = 0;
-            for (int i = 0; i < L.n; i++) {
+            for (int i = i0; i < i1; i++) {
                 const int off = L.step * mnr;
                 const int rx = L.high ? bx0 + off : bx0 + i;
                 const int ry = L.high ? by0 + i : by0 + off;
@@ -853,28 +856,20 @@ hipError_t launch_ref_endpoints(Ctx& c, int W, int H, const sva_camera& cref,
     return hipGetLastError();
 }
 
-// The plane kernel's tiles and workgroups: whole tiles fill as many full
-// rounds of the chip's workgroup slots as they can, and the tiles left over
-// for a last, partial round are split into the most shares (up to
-// kPlaneSplitMax) that still fit one round -- so the last round ends with
-// short shares instead of a few whole tiles on an idle chip.  Frames with
-// fewer tiles than slots (640x480: 140 tiles for 768 slots) split them all.
-struct PlaneGrid {
-    int t1;     // whole tiles
-    int nsh;    // shares per later tile (1: no split)
-};
-static PlaneGrid plane_grid(long long tiles, int cu_count) {
+// Shares per tile: about four rounds of the chip's workgroup slots in all,
+// rounded, within [kPlaneSplitMin, kPlaneSplitMax] -- 1080p (990 tiles, 768
+// slots), 1440p and 4K 3, 1280x720 and smaller 6.  Measured with every tile
+// split S ways (profiles/r05_v5/plane_walk/n*_*.log.txt, r6q/): the shares
+// fill the last round and balance the uneven tile work (a Low pair's tiles
+// near the image border carry fewer planes); more shares than that pay more
+// per-share setup than they save.
+static int plane_shares(long long tiles, int cu_count) {
     const long long slots = (long long)cu_count * tune::kPlaneMinBlocks;
-    PlaneGrid g{(int)tiles, 1};
-    if (tune::kPlaneSplitMax <= 1 || slots <= 0) return g;
-    const long long t1 = tiles / slots * slots, rest = tiles - t1;
-    if (rest == 0) return g;
-    long long s = slots / rest;
+    if (tune::kPlaneSplitMax <= 1 || slots <= 0 || tiles <= 0) return 1;
+    long long s = (tune::kPlaneSplitRounds * slots + tiles / 2) / tiles;
     if (s > tune::kPlaneSplitMax) s = tune::kPlaneSplitMax;
-    if (s < 2) return g;
-    g.t1 = (int)t1;
-    g.nsh = (int)s;
-    return g;
+    if (s < tune::kPlaneSplitMin) s = tune::kPlaneSplitMin;
+    return (int)s;
 }
 
 hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, int W, int H,
@@ -887,15 +882,14 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
     // offset-plane algorithm for every k (sva_api checks 1 <= k <= 32)
     const int gx = (W - 2 * k + 63) / 64, gy = (H - 2 * k + P3_ROWS - 1) / P3_ROWS;
     const long long tiles = (long long)gx * gy;
-    PlaneGrid pg = plane_grid(tiles, c.cu_count);
+    int nsh = plane_shares(tiles, c.cu_count);
     // test hook: SVA_PLANE_SPLIT=n splits every tile into n shares (1..16),
-    // so the parity tests cover the split route at every size
+    // so the parity tests cover every share count at every size
     if (const char* e = std::getenv("SVA_PLANE_SPLIT")) {
         const int n = std::atoi(e);
-        if (n >= 1 && n <= 16) pg = n > 1 ? PlaneGrid{0, n} : PlaneGrid{(int)tiles, 1};
+        if (n >= 1 && n <= 16) nsh = n;
     }
-    const bool split = pg.nsh > 1 && pg.t1 < tiles;
-    const long long nblk = pg.t1 + (tiles - pg.t1) * (split ? pg.nsh : 1);
+    const bool split = nsh > 1;
     unsigned* keys = nullptr;
     if (split) {
         hipError_t e = c.ref_keys.ensure((size_t)W * H * sizeof(unsigned));
@@ -904,12 +898,12 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
         e = hipMemsetAsync(keys, 0xff, (size_t)W * H * sizeof(unsigned), c.stream);
         if (e != hipSuccess) return e;
     }
-    const dim3 pg3((unsigned)nblk);
+    const dim3 pg3((unsigned)nsh, (unsigned)gx, (unsigned)gy);
 #define SVA_PLANE3_CASE(K_)                                                                    \
     case K_:                                                                                   \
         hipLaunchKernelGGL(ref_plane3_kernel<K_>, pg3, dim3(256), 0, c.stream, ref, other, W, H, \
                            pitch, mask, (const int4*)ends, valid_in, disp_u8, disp_u16,         \
-                           valid_out, keys, gx, pg.t1, pg.nsh);                                \
+                           valid_out, keys);                                                   \
         break;
     switch (k) {
         SVA_PLANE3_CASE(1) SVA_PLANE3_CASE(2) SVA_PLANE3_CASE(3) SVA_PLANE3_CASE(4)

@@ -241,22 +241,34 @@ constexpr int kPlaneNoHoistDiv = 0;
 // outer offset, instead of eight VGPRs held across the plane loop (1), at
 // every k whose LDS still leaves kPlaneMinBlocks workgroups per CU.
 constexpr int kPlanePoLds = 1;
-// The tiles left over for the plane kernel's last, partial round of
-// workgroup slots (all of them when a frame has fewer tiles than slots) are
-// split into up to kPlaneSplitMax shares of their offsets, each its own
-// workgroup; the per-pixel keys meet in global memory by atomicMin
-// (refpath.hip plane_grid, ref_finalize_kernel).  kPlaneSplitInner: shares
-// of the inner offsets (1), of the outer offsets (0), or per tile by its
-// offset box (2).  ref_match ms, in-process, unsplit / inner / outer, every
-// tile split (profiles/r05_v5/plane_split/): 960x540 12->11 0.216 / 0.157 /
-// 0.178, 12->7 0.209 / 0.153 / 0.177, 12->6 0.298 / 0.194 / 0.185, 12->18
-// 0.278 / 0.185 / 0.176; 640x480 12->11 0.147 / 0.091 / 0.104, 12->6 0.205 /
-// 0.106 / 0.098; at 1080p every tile split gave -9 % (12->11) to +4 %
-// (12->7), the reason only the last round's tiles are split there.
+// Every tile of the plane kernel is split into S shares of its offsets, each
+// its own workgroup; the per-pixel keys meet in global memory by atomicMin
+// (refpath.hip plane_shares, ref_finalize_kernel).  S = kPlaneSplitRounds
+// rounds of workgroup slots over the tile count, rounded, within
+// [kPlaneSplitMin, kPlaneSplitMax].  kPlaneSplitInner: shares of the inner offsets (1), of the
+// outer offsets (0), or per tile by its offset box (2).  ref_match ms,
+// in-process, unsplit / inner / outer, every tile split
+// (profiles/r05_v5/plane_split/): 960x540 12->11 0.216 / 0.157 / 0.178,
+// 12->7 0.209 / 0.153 / 0.177, 12->6 0.298 / 0.194 / 0.185, 12->18 0.278 /
+// 0.185 / 0.176; 640x480 12->11 0.147 / 0.091 / 0.104, 12->6 0.205 / 0.106 /
+// 0.098.  With the ranged bitmap walk (kPlaneWalkRange) every share count
+// S = 1 / 2 / 3 / 4 / 6, ms for 12->11 + 12->6 (profiles/r05_v5/plane_walk/
+// n*): 1080p 1.539 / 1.408 / 1.343 / 1.363 / 1.423; 1280x720 0.699 / 0.589 /
+// 0.541 / 0.563 / 0.549; 960x540 0.514 / 0.355 / 0.319 / 0.304 / 0.311;
+// 640x480 0.354 / 0.245 / 0.192 / 0.190 / 0.169.  S = 1 / 2 / 3 (r6q):
+// 2560x1440 3.383 / 3.206 / 2.832; 3840x2160 9.190 / 8.803 / 8.590 (the
+// round-based rule alone gave S = 1 at 4K, 2.3-4.7 % slower than the
+// previous split band).
+constexpr int kPlaneSplitMin = 3;
 constexpr int kPlaneSplitMax = 6;
+constexpr int kPlaneSplitRounds = 4;
 constexpr int kPlaneSplitInner = 2;
-// The split tiles: a band in the middle of the frame (1) or the last tiles (0).
-constexpr int kPlaneSplitMiddle = 1;
+// The plane bitmap walk visits only a line's points whose major-axis
+// coordinate falls in the pass's outer range or the share's inner range (1),
+// or every point of every distinct line (0).  Without it every share re-walks
+// whole lines: 1080p 12->11 with 3 shares 0.728 -> 0.671 ms, 12->7 0.653 ->
+// 0.598 (profiles/r05_v5/plane_walk/r_3_*).
+constexpr int kPlaneWalkRange = 1;
 
 }  // namespace tune
 }  // namespace sva
