@@ -376,10 +376,23 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     if (t < 6) box[t] = t >= 4 ? 0 : ((t & 1) ? -0x7fffffff : 0x7fffffff);
     // R region, column-major; rows up to the stride are staged as well (read
     // into registers below, masked out of every sum)
-    for (int i = t; i < RW * RS; i += 256) {
-        const int v = i / RW, u = i - v * RW;
-        const int gx = rx0 + u, gy = ry0 + v;
-        RT[u * RS + v] = (gx < W && gy < H) ? ref[(size_t)gy * pitch + gx] : 0;
+    // (eight byte loads in flight per thread, from clamped in-image
+    // addresses, then the eight LDS stores: a branch per byte had made every
+    // load its own load-wait-store round trip)
+    for (int i0 = 0; i0 < RW * RS; i0 += 8 * 256) {
+        unsigned bv[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int i = i0 + q * 256 + t;
+            const int v = i / RW, u = i - v * RW;
+            bv[q] = ref[(size_t)min(ry0 + v, H - 1) * pitch + min(rx0 + u, W - 1)];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int i = i0 + q * 256 + t;
+            const int v = i / RW, u = i - v * RW;
+            if (i < RW * RS) RT[u * RS + v] = (rx0 + u < W && ry0 + v < H) ? (uint8_t)bv[q] : 0;
+        }
     }
     // this thread's pixels: column tx0 + lane, rows ty0 + r0 + j
     int ox[8], oy[8], pa[8], pn[8];
