@@ -2,7 +2,7 @@
 # Round-5 final measurements at HEAD (Mode R every tile split + ranged walk): suite, smoke, benches, rocprof
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/r5final4
+O=gpurun_out/r5final5
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest tests -q -m gpu -rf --timeout 300 --timeout-method thread > $O/pytest_gpu_all.log 2>&1; rc=$?
