@@ -223,7 +223,9 @@ int sva_wta_d(void* ctx, const uint16_t* S, int width, int height, const sva_sgm
  * Bresenham candidates (functions.cpp:253-321), 2k x 2k SAD (getAbsDiff,
  * functions.cpp:215-218), first-minimum WTA (:85), (uchar)(int)norm (:89).
  * mask: W*H u8 or NULL (all selected, :53).  Writes only pixels the pair keeps
- * (multi-pair callers overwrite in order, :55); disp_u16 / valid nullable. */
+ * (multi-pair callers overwrite in order, :55); disp_u16 / valid nullable.
+ * The context keeps a W*H u32 key buffer (grown on demand, freed by
+ * sva_destroy) where a tile's workgroups merge their first minima. */
 int sva_disparity_ref(void* ctx, const uint8_t* ref_img, const uint8_t* other_img, int width,
                       int height, size_t pitch, const uint8_t* mask,
                       const sva_camera* ref_cam, const sva_camera* other_cam, int k,
