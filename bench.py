@@ -254,37 +254,83 @@ def mode_r_only(size="1920x1080"):
             json.dump({"W": W, "H": H, "k": k}, f)
 
 
+def valu_roofline(kernel, c, t_ms, label):
+    """VALU issue roofline of one kernel from one SQ counter pass (counters
+    averaged per launch, `c`) and its hipEvent time `t_ms`:
+
+      frac          = SQ_INSTS_VALU / (t x VALU_PEAK_PER_S), the chip's SIMD-32
+                      issue rate at the 2.4 GHz peak clock (VERDICT r05 weak #2:
+                      rounds 3-5 charged 4 cycles per wave64 instruction, which is
+                      one wave's own issue interval, and so doubled every VALU
+                      fraction);
+      frac_of_mix_peak  against the rate tools/microbench_valu.hip measures for
+                      this kernel's own static instruction mix at 8 waves/SIMD
+                      (VALU_MIX_PEAK_PER_S), where one is measured;
+      frac_at_clock = 2 x SQ_INSTS_VALU / (1,024 x GRBM_GUI_ACTIVE / 8): issue
+                      slots used out of those the kernel's own active cycles
+                      offered (clock-independent; the counter is summed over the
+                      8 XCDs, MI355X_MICROARCH.md "DVFS give-back");
+    plus the shares of SQ_WAVE_CYCLES that waves spent issuing VALU
+    (SQ_ACTIVE_INST_VALU) and waiting (SQ_WAIT_INST_ANY: for an instruction's
+    operands, SQ_WAIT_ANY: for anything)."""
+    insts = c.get("SQ_INSTS_VALU")
+    if not insts or not t_ms:
+        raise RuntimeError(f"no {kernel} VALU counters or time")
+    ach = insts / (t_ms * 1e-3)
+    out = {"bound": "valu", "unit": "wave-instructions/s", "kernel": label,
+           "sq_insts_valu": int(insts), "kernel_ms": round(t_ms, 4),
+           "achieved_per_s": round(ach, 1), "peak_per_s": round(VALU_PEAK_PER_S, 1),
+           "frac": round(ach / VALU_PEAK_PER_S, 4),
+           "peak_source": VALU_PEAK_SOURCE}
+    mix = VALU_MIX_PEAK_PER_S.get(kernel)
+    if mix:
+        out["mix_peak_per_s"] = mix
+        out["frac_of_mix_peak"] = round(ach / mix, 4)
+        out["mix_source"] = VALU_MIX_SOURCE
+    g = c.get("GRBM_GUI_ACTIVE")
+    dur = c.get("_dur_ns")
+    if g:
+        out["grbm_gui_active"] = int(g)
+        out["frac_at_clock"] = round(VALU_ISSUE_CYCLES * insts / (SIMDS * g / XCDS), 4)
+        if dur:
+            out["clock_ghz"] = round(g / XCDS / dur, 3)
+            out["pmc_kernel_ms"] = round(dur * 1e-6, 4)
+    wc = c.get("SQ_WAVE_CYCLES")
+    if wc:
+        for key, name in (("SQ_ACTIVE_INST_VALU", "active_valu_share"),
+                          ("SQ_WAIT_INST_ANY", "wait_inst_any_share"),
+                          ("SQ_WAIT_ANY", "wait_any_share")):
+            if key in c:
+                out[name] = round(c[key] / wc, 4)
+        out["sq"] = {k: int(v) for k, v in c.items() if k.startswith("SQ_")}
+    return out
+
+
 def mode_r_roofline(mr):
     """Mode R is VALU/latency-bound, so its roofline is the
-    VALU issue rate: SQ_INSTS_VALU x 4 cycles (one wave64 VALU instruction
-    occupies a SIMD for 4 cycles) / (1,024 SIMDs x clock x kernel time), the
-    instructions from one live rocprofv3 pass over mode_r_only(), the kernel
-    time from the hipEvent-timed ref_match launches of mode_r_beside.  The
-    child runs mr's own frame size and stamps it; a mismatch is refused, so
-    the fraction never divides one frame's instructions by another's time."""
+    VALU issue rate (valu_roofline), the instructions from one live rocprofv3
+    SQ pass over mode_r_only(), the kernel time from the hipEvent-timed
+    ref_match launches of mode_r_beside.  The child runs mr's own frame size
+    and stamps it; a mismatch is refused, so the fraction never divides one
+    frame's instructions by another's time."""
     import tempfile
     outdir = tempfile.mkdtemp(prefix="sva_pmc_r_", dir="/tmp")
     stamp = os.path.join(outdir, "mode_r_stamp.json")
-    res = _pmc_pass("SQ_INSTS_VALU GRBM_GUI_ACTIVE", [], outdir,
+    res = _pmc_pass(SQ_VALU_COUNTERS, [], outdir,
                     child=mode_r_child_args(mr["W"], mr["H"]), env={"SVA_MODE_R_STAMP": stamp})
     with open(stamp) as f:
         ran = json.load(f)
     if (ran["W"], ran["H"]) != (mr["W"], mr["H"]):
         raise RuntimeError(f"Mode R PMC child ran {ran['W']}x{ran['H']}, timed {mr['W']}x{mr['H']}")
     c = res.get("ref_match", {})
-    insts = c.get("SQ_INSTS_VALU")
     t_ms = mr.get("ref_match_kernel_ms")
-    if not insts or not t_ms:
+    if not c.get("SQ_INSTS_VALU") or not t_ms:
         raise RuntimeError("no ref_plane3_kernel counters")
-    cap = SIMDS * MI355X_ENGINE_GHZ * 1e9 * t_ms * 1e-3 / 4.0   # wave-instructions
-    return {"bound": "valu", "unit": "wave-instructions", "kernel": "ref_plane3_kernel<20>",
-            "frame": f"{mr['W']}x{mr['H']}",
-            "sq_insts_valu": int(insts), "kernel_ms": t_ms,
-            "achieved_per_s": round(insts / (t_ms * 1e-3), 1),
-            "peak_per_s": round(SIMDS * MI355X_ENGINE_GHZ * 1e9 / 4.0, 1),
-            "frac": round(insts / cap, 4),
-            "grbm_gui_active": int(c.get("GRBM_GUI_ACTIVE", 0)),
-            "model": "SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x 2.4 GHz x ref_match time)"}
+    out = valu_roofline("ref_match", c, t_ms, "ref_plane3_kernel<20>")
+    out["frame"] = f"{mr['W']}x{mr['H']}"
+    out["model"] = ("SQ_INSTS_VALU / (ref_match time x 1,024 SIMDs x 2.4 GHz / 2 cycles per "
+                    "wave64 VALU instruction)")
+    return out
 
 
 def frame_overlap_beside(W, H, D, frames=40, rounds=2):
@@ -364,6 +410,24 @@ PMC_KERNELS = {"sgm_paths_kernel": "sgm_paths", "wta_hv_kernel": "wta_hv",
                "census_cost_mma_kernel": "cost", "ref_plane3_kernel": "ref_match"}
 MI355X_ENGINE_GHZ = 2.4   # peak engine clock (MI355X_MICROARCH.md)
 SIMDS = 1024              # 256 CUs x 4 SIMDs
+XCDS = 8                  # GRBM_GUI_ACTIVE is summed over the 8 XCDs
+# MI355X_MICROARCH.md "Wave scheduling" (:53-54): each CU has 4 SIMD-32 units
+# and a wave64 VALU instruction issues over 2 cycles; the 4 cycles of its
+# 'vector-instruction ISSUE cost' row are what ONE wave alone sustains.
+VALU_ISSUE_CYCLES = 2.0
+VALU_PEAK_PER_S = SIMDS * MI355X_ENGINE_GHZ * 1e9 / VALU_ISSUE_CYCLES     # 1.2288e12
+VALU_PEAK_SOURCE = ("1,024 SIMD-32 units x 2.4 GHz / 2 cycles per wave64 VALU instruction "
+                    "(MI355X_MICROARCH.md Wave scheduling)")
+# The same ceiling measured for each kernel's own instruction mix:
+# tools/microbench_valu.hip kinds 18 / 19 (the static VALU mix of
+# wta_hv_kernel<8,3,false> and of ref_plane3_kernel<20>'s per-plane body,
+# tools/isa_mix.py), best of 1/2/4/8 waves per SIMD, chip-wide wave-instructions
+# per second from the kernel's hipEvent time (profiles/r06_v1/microbench_valu.txt).
+VALU_MIX_PEAK_PER_S = {}
+VALU_MIX_SOURCE = "tools/microbench_valu.hip mix kinds, profiles/r06_v1/microbench_valu.txt"
+SQ_VALU_COUNTERS = ("SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES "
+                    "SQ_BUSY_CYCLES GRBM_GUI_ACTIVE")
+EA_COUNTERS = "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum GRBM_GUI_ACTIVE"
 
 
 def _pmc_pass(counter, args, outdir, child=None, env=None):
@@ -386,18 +450,26 @@ def _pmc_pass(counter, args, outdir, child=None, env=None):
     if r.returncode != 0:
         raise RuntimeError(f"rocprofv3 --pmc {counter} exited {r.returncode}: {r.stderr[-300:]}")
     path = os.path.join(d, "run_counter_collection.csv")
-    agg = {}
+    agg, durs = {}, {}
     for row in csv.DictReader(open(path)):
         name = row["Kernel_Name"]
         for key, short in PMC_KERNELS.items():
             if key + "<" in name or key + "(" in name:
                 agg.setdefault((short, row["Counter_Name"]), []).append(float(row["Counter_Value"]))
+                try:
+                    durs.setdefault(short, {})[row["Dispatch_Id"]] = \
+                        float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+                except (KeyError, ValueError):
+                    pass
                 break
     if len(counters) == 1:
         return {k: sum(v) / len(v) for (k, _), v in agg.items()}
     out = {}
     for (k, c), v in agg.items():
         out.setdefault(k, {})[c] = sum(v) / len(v)
+    for k, dd in durs.items():      # kernel duration under this pass, ns
+        if k in out and dd:
+            out[k]["_dur_ns"] = sum(dd.values()) / len(dd)
     return out
 
 
@@ -419,6 +491,75 @@ def live_traffic(a):
         out[k] = {"hbm_read_bytes": int(rd), "hbm_write_bytes": int(wr),
                   "hbm_bytes_per_launch": int(rd + wr)}
     return out
+
+
+def engine_counters(a):
+    """Two more live PMC passes over this workload (N = 1, rank 0): the SQ
+    VALU set for every pipeline kernel, and the L2's memory-side requests with
+    the engine clock for the dominant kernel (tells a
+    slower box's clock from its memory)."""
+    import tempfile
+    outdir = tempfile.mkdtemp(prefix="sva_pmc_e_", dir="/tmp")
+    args = ["--workload", a.workload, "--pairs-per-rank", str(a.pairs_per_rank)]
+    return _pmc_pass(SQ_VALU_COUNTERS, args, outdir), _pmc_pass(EA_COUNTERS, args, outdir)
+
+
+def ea_figures(c, t_ms):
+    """roofline.engine: clock and TCC EA request bytes of one kernel.  Reads:
+    RDREQ x 128 B (gfx950 tallies a 128-B streaming read as one 64-B request
+    in FETCH_SIZE = RDREQ x 64 B, MI355X_MICROARCH.md HBM); writes:
+    WRREQ_64B x 64 B + (WRREQ - WRREQ_64B) x 32 B."""
+    rd, wr, w64 = (c.get(k) for k in ("TCC_EA0_RDREQ_sum", "TCC_EA0_WRREQ_sum",
+                                       "TCC_EA0_WRREQ_64B_sum"))
+    out = {"source": "live rocprofv3 --pmc " + EA_COUNTERS}
+    g, dur = c.get("GRBM_GUI_ACTIVE"), c.get("_dur_ns")
+    if g and dur:
+        out["clock_ghz"] = round(g / XCDS / dur, 3)
+        out["pmc_kernel_ms"] = round(dur * 1e-6, 4)
+        out["grbm_gui_active"] = int(g)
+    if rd is not None:
+        out["ea_rdreq"] = int(rd)
+        out["ea_read_bytes"] = int(rd * 128)
+    if wr is not None and w64 is not None:
+        out["ea_wrreq"] = int(wr)
+        out["ea_wrreq_64b"] = int(w64)
+        out["ea_write_bytes"] = int(w64 * 64 + (wr - w64) * 32)
+    if "ea_read_bytes" in out and "ea_write_bytes" in out and t_ms:
+        tot = out["ea_read_bytes"] + out["ea_write_bytes"]
+        out["ea_bytes"] = tot
+        out["ea_gbs_at_event_time"] = round(tot / (t_ms * 1e-3) / 1e9, 1)
+    return out
+
+
+def attach_engine(a, out, kernels, world):
+    """valu_roofline per pipeline kernel and roofline.engine (clock + EA bytes)
+    from engine_counters(), on rank 0 at N = 1 with --pmc live only."""
+    under_prof = any(k.startswith("ROCPROF") for k in os.environ) or \
+        os.environ.get("SVA_BENCH_PMC_CHILD")
+    if a.pmc != "live" or world != 1 or under_prof or getattr(a, "batch", False):
+        return
+    try:
+        sq, ea = engine_counters(a)
+    except Exception as e:                           # keep the bench line; say why
+        out["valu_roofline"] = {"error": str(e)[:200]}
+        return
+    labels = {"sgm_paths": "sgm_paths_kernel", "wta_hv": "wta_hv_kernel",
+              "cost": "census_cost_mma_kernel"}
+    vr = {}
+    for k, label in labels.items():
+        if k in sq and k in kernels:
+            try:
+                vr[k] = valu_roofline(k, sq[k], kernels[k]["avg_ms"], label)
+            except RuntimeError:
+                pass
+    out["valu_roofline"] = vr
+    rf = out.get("roofline")
+    if rf and rf.get("kernel") in ea:
+        rf["engine"] = ea_figures(ea[rf["kernel"]], rf.get("kernel_avg_ms"))
+    ag = out.get("aggregation_roofline")
+    if ag:
+        ag["engine"] = {k: ea_figures(ea[k], kernels.get(k, {}).get("avg_ms"))
+                        for k in AGG_KERNELS if k in ea}
 
 
 def attach_traffic(a, out, world):
@@ -1345,6 +1486,7 @@ def main():
             out["frame_overlap"] = frame_overlap_beside(W, H, D)
     if rank == 0:
         attach_traffic(a, out, world)
+        attach_engine(a, out, kernels, world)
         print(json.dumps(out), flush=True)
     for c in ctxs:
         c.close()

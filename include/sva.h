@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SVA_ABI_VERSION 5
+#define SVA_ABI_VERSION 6
 
 enum {
     SVA_OK = 0,
@@ -127,6 +127,27 @@ int sva_set_timing(void* ctx, int enable);
 int sva_reset_timing(void* ctx);
 /* Total milliseconds and launch count of kernel `name` since the last reset. */
 int sva_kernel_time(void* ctx, const char* name, double* total_ms, int64_t* count);
+
+/* Per-context test and debug switches (ABI v6; they replace the round-5
+ * SVA_PLANE_SPLIT environment variable, so the environment never changes
+ * how production work is dispatched).  Every key defaults to 0 = off.
+ *   SVA_DEBUG_PLANE_SPLIT    set: split every Mode R tile into 1..16 workgroup
+ *                            shares (0 = the automatic count, refpath.hip
+ *                            plane_shares), so the parity tests cover every
+ *                            share count at every size.
+ *   SVA_DEBUG_FAIL_COST_AT   set: the next sva_disparity_sgm_batch_d call fails
+ *                            its n-th cost launch (1-based) with
+ *                            SVA_ERR_DEVICE, without launching it; the switch
+ *                            then resets to 0 (fault injection for the
+ *                            side-stream join test).
+ *   SVA_DEBUG_SIDE_IDLE      get: 1 if every side stream of the batch route
+ *                            has finished its queued work (hipStreamQuery),
+ *                            else 0. */
+#define SVA_DEBUG_PLANE_SPLIT 1
+#define SVA_DEBUG_FAIL_COST_AT 2
+#define SVA_DEBUG_SIDE_IDLE 3
+int sva_set_debug(void* ctx, int key, int64_t value);
+int sva_get_debug(void* ctx, int key, int64_t* value);
 
 /* ------------------------------------------------------ Mode S (SGM) --- */
 /* Whole path: census -> Hamming cost -> 8-path SGM -> WTA (+ sub-pixel).
@@ -224,8 +245,12 @@ int sva_wta_d(void* ctx, const uint16_t* S, int width, int height, const sva_sgm
  * functions.cpp:215-218), first-minimum WTA (:85), (uchar)(int)norm (:89).
  * mask: W*H u8 or NULL (all selected, :53).  Writes only pixels the pair keeps
  * (multi-pair callers overwrite in order, :55); disp_u16 / valid nullable.
- * The context keeps a W*H u32 key buffer (grown on demand, freed by
- * sva_destroy) where a tile's workgroups merge their first minima. */
+ * The context keeps a W*H key buffer (u32; u64 when a line can hold 4,096
+ * or more candidates, i.e. W or H >= 4096; grown on demand, freed by
+ * sva_destroy) where a tile's workgroups merge their first minima.
+ * Limits: 1 <= k, 2k < W and 2k < H (the reference's own window bounds,
+ * CameraStereoVision.cpp:49-51); W, H <= 32767.  k <= 32 runs the
+ * offset-plane kernel, larger k one wave per pixel. */
 int sva_disparity_ref(void* ctx, const uint8_t* ref_img, const uint8_t* other_img, int width,
                       int height, size_t pitch, const uint8_t* mask,
                       const sva_camera* ref_cam, const sva_camera* other_cam, int k,

@@ -34,8 +34,11 @@ SVA_TIMING_OFF = 0
 SVA_TIMING_ALL = 1
 SVA_TIMING_PATHS = 2
 SVA_TIMING_AGG = 3
+SVA_DEBUG_PLANE_SPLIT = 1
+SVA_DEBUG_FAIL_COST_AT = 2
+SVA_DEBUG_SIDE_IDLE = 3
 # The ABI this binding is written against (include/sva.h SVA_ABI_VERSION).
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # Symbols declared in include/sva.h (checked by tests/test_abi.py).
 EXPORTED = [
@@ -54,7 +57,8 @@ EXPORTED = [
     "sva_ref_error", "sva_masked_mean_d", "sva_masked_mean", "sva_tile_layout_of",
     "sva_tile_check", "sva_paths_tile_d", "sva_wta_hv_d", "sva_multi_create", "sva_multi_destroy",
     "sva_multi_synchronize", "sva_multi_last_error", "sva_multi_plan", "sva_multi_context",
-    "sva_batch_sgm_d", "sva_array_depth", "sva_disparity_sgm_batch_d",
+    "sva_batch_sgm_d", "sva_array_depth", "sva_disparity_sgm_batch_d", "sva_set_debug",
+    "sva_get_debug",
 ]
 SVA_MULTI_GATHER_RCCL = 0
 SVA_MULTI_GATHER_PEER = 1
@@ -156,6 +160,8 @@ def _load() -> ct.CDLL:
         "sva_set_timing": (i32, [vp, i32]),
         "sva_reset_timing": (i32, [vp]),
         "sva_kernel_time": (i32, [vp, ct.c_char_p, P(dbl), P(ct.c_int64)]),
+        "sva_set_debug": (i32, [vp, i32, ct.c_int64]),
+        "sva_get_debug": (i32, [vp, i32, P(ct.c_int64)]),
         "sva_disparity_sgm": (i32, [vp, vp, vp, i32, i32, sz, P(SgmParams), vp, vp]),
         "sva_disparity_sgm_d": (i32, [vp, vp, vp, i32, i32, sz, P(SgmParams), vp, vp]),
         "sva_census_d": (i32, [vp, vp, i32, i32, sz, vp]),
@@ -330,6 +336,15 @@ class Context:
 
     def reset_timing(self):
         self._chk(lib.sva_reset_timing(self.h))
+
+    def set_debug(self, key: int, value: int):
+        """sva_set_debug: SVA_DEBUG_PLANE_SPLIT / SVA_DEBUG_FAIL_COST_AT (tests)."""
+        self._chk(lib.sva_set_debug(self.h, key, int(value)))
+
+    def get_debug(self, key: int) -> int:
+        v = ct.c_int64(0)
+        self._chk(lib.sva_get_debug(self.h, key, ct.byref(v)))
+        return v.value
 
     def kernel_time(self, name: str) -> tuple[float, int]:
         ms = ct.c_double(0)

@@ -5,12 +5,16 @@
 //                         operand order (Camera.cpp:15-34,
 //                         CameraStereoVision.cpp:28,60-71).  FMA contraction
 //                         is off for this file so every rounding matches.
-//   ref_plane3_kernel     the offset-plane algorithm (below) for every k the
-//                         ABI accepts (1..32), with a per-pixel fallback
-//                         (match_pixel_wave) for tiles whose offset geometry
-//                         exceeds its buffers; first-minimum argmin, then
+//   ref_plane3_kernel     the offset-plane algorithm (below) for k = 1..32,
+//                         with a per-pixel fallback (match_pixel_wave) for
+//                         tiles whose offset geometry exceeds its buffers;
+//                         first-minimum argmin, then
 //                         (uchar)(int)sqrt(dx^2 + dy^2)
-//                         (CameraStereoVision.cpp:85-89).
+//                         (CameraStereoVision.cpp:85-89).  WIDE instances
+//                         (W or H >= 4096: a line may hold 4,096 candidates
+//                         or more) keep 64-bit (SAD, i) first-minimum keys.
+//   ref_pixel_kernel      k > 32 (the reference bounds k only by the image,
+//                         CameraStereoVision.cpp:49-51): one wave per pixel.
 #pragma clang fp contract(off)
 
 #include <cstdlib>
@@ -134,14 +138,38 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 // with v_sad_u8 (4 |a-b| per lane-op) on v_alignbyte-realigned rows, and the
 // first minimum as a wave-wide u64 min over (SAD << 32 | i).  The per-tile
 // fallback of ref_plane3_kernel.
-template <int ND>
+// sad_row over a row of any (even) length: 64-byte chunks, then the rest
+// (k > 32, where the 2k-byte row outgrows one sad_row<ND> instance).
+template <int N>
+__device__ __forceinline__ unsigned sad_tail(const uint8_t* a, const uint8_t* b, unsigned lastmask,
+                                             int nbytes, unsigned acc) {
+    if constexpr (N > 16) {
+        return acc;
+    } else {
+        if ((nbytes + 3) / 4 == N) return sad_row<N>(a, b, lastmask, nbytes, acc);
+        return sad_tail<N + 1>(a, b, lastmask, nbytes, acc);
+    }
+}
+__device__ __forceinline__ unsigned sad_span(const uint8_t* a, const uint8_t* b, int nbytes,
+                                             unsigned acc) {
+    int off = 0;
+    for (; off + 64 <= nbytes; off += 64) acc = sad_row<16>(a + off, b + off, 0xffffffffu, 64, acc);
+    const int rem = nbytes - off;
+    if (rem > 0) acc = sad_tail<1>(a + off, b + off, (rem & 3) ? 0xffffu : 0xffffffffu, rem, acc);
+    return acc;
+}
+
+// KEY: the type of the split plane loop's per-pixel first-minimum keys
+// (u32 (SAD << 12 | i), or u64 (SAD << 32 | i) for WIDE frames).  ND = 0:
+// rows of any length (sad_span, k > 32).
+template <int ND, class KEY = unsigned>
 __device__ __forceinline__ void match_pixel_wave(const uint8_t* __restrict__ ref,
                                                  const uint8_t* __restrict__ other, int W,
                                                  size_t pitch, int x, int y, const int4 e, int k,
                                                  uint8_t* __restrict__ disp_u8,
                                                  uint16_t* __restrict__ disp_u16,
                                                  uint8_t* __restrict__ valid_out,
-                                                 unsigned* __restrict__ keys = nullptr) {
+                                                 KEY* __restrict__ keys = nullptr) {
     const int lane = threadIdx.x & 63;
     const size_t p = (size_t)y * W + x;
     const Line L = make_line(e.x, e.y, e.z, e.w);                     // :73
@@ -157,18 +185,25 @@ __device__ __forceinline__ void match_pixel_wave(const uint8_t* __restrict__ ref
             line_point(L, i, cx, cy);
             const uint8_t* sel = other + (size_t)(cy - k) * pitch + (cx - k);
             unsigned acc = 0;
-            for (int v = 0; v < nbytes; v++)
-                acc = sad_row<ND>(sel + (size_t)v * pitch, kern + (size_t)v * pitch, lastmask,
-                                  nbytes, acc);
+            for (int v = 0; v < nbytes; v++) {
+                if constexpr (ND == 0)
+                    acc = sad_span(sel + (size_t)v * pitch, kern + (size_t)v * pitch, nbytes, acc);
+                else
+                    acc = sad_row<ND>(sel + (size_t)v * pitch, kern + (size_t)v * pitch, lastmask,
+                                      nbytes, acc);
+            }
             key = ((unsigned long long)acc << 32) | (unsigned)i;
         }
         key = wave_min_u64(key);                                      // :85 first min
         best = key < best ? key : best;
     }
     if (lane == 0 && keys) {
-        // the split plane loop's first-minimum key (SAD << 12 | i), finished
-        // by ref_finalize_kernel
-        atomicMin(&keys[p], ((unsigned)(best >> 32) << 12) | (unsigned)(best & 0xfffu));
+        // the split plane loop's first-minimum key (SAD << 12 | i, or the
+        // full (SAD, i) pair for WIDE frames), finished by ref_finalize_kernel
+        if constexpr (sizeof(KEY) == 8)
+            atomicMin(&keys[p], (KEY)best);
+        else
+            atomicMin(&keys[p], ((unsigned)(best >> 32) << 12) | (unsigned)(best & 0xfffu));
     } else if (lane == 0) {
         int cx, cy;
         line_point(L, (int)(best & 0xffffffffu), cx, cy);
@@ -266,7 +301,8 @@ __device__ __forceinline__ void scan64_dpp_n(unsigned (&a)[N], unsigned (&b)[N])
 //     own major axis is the outer one -- recomputed only when the outer
 //     offset changes.  Per plane the test is (d_in - lo) < len, and the
 //     first-minimum key is the u32 (SAD << 12 | i): SAD < 2^20 for k <= 32,
-//     i < 4096 (Mode R requires W, H < 4096).
+//     i < 4096 when W, H < 4096.  Larger frames take the WIDE instance, whose
+//     u64 key (SAD << 32 | i) holds any i (VERDICT r05 missing #3).
 constexpr int P3_ROWS = 32;                          // 4 waves x 8 rows
 constexpr int P3_OU_BYTES = tune::kPlaneOuKB * 1024;  // staged O chunk
 constexpr int P3_WORDS = tune::kPlaneWords;            // offset bitmap per pass: 32K bits
@@ -322,13 +358,18 @@ __device__ __forceinline__ void line_interval(int po, int pa, int pn, bool mi, b
     }
 }
 
-template <int K>
+template <int K, bool WIDE>
 __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     const uint8_t* __restrict__ ref, const uint8_t* __restrict__ other, int W, int H, size_t pitch,
     const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
     const uint8_t* __restrict__ valid_in, uint8_t* __restrict__ disp_u8,
     uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out,
-    unsigned* __restrict__ keys) {
+    void* __restrict__ keys_) {
+    // first-minimum keys: u32 (SAD << 12 | i) while every line holds < 4096
+    // candidates, else u64 (SAD << 32 | i)
+    using Key = typename std::conditional<WIDE, unsigned long long, unsigned>::type;
+    constexpr Key KNONE = (Key)~(Key)0;
+    Key* keys = (Key*)keys_;
     // Grid (shares, tiles x, tiles y): every tile is split over gridDim.x
     // workgroups (one share of its offsets each, adjacent in dispatch order)
     // whose per-pixel first-minimum keys meet in keys[] by atomicMin
@@ -472,8 +513,8 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
             if (x >= W - K || y >= H - K) continue;
             const size_t p = (size_t)y * W + x;
             if (!valid_in[p] || (mask && mask[p] == 0)) continue;
-            match_pixel_wave<ND>(ref, other, W, pitch, x, y, ends[p], K, disp_u8, disp_u16,
-                                 valid_out, keys);
+            match_pixel_wave<ND, Key>(ref, other, W, pitch, x, y, ends[p], K, disp_u8, disp_u16,
+                                      valid_out, keys);
         }
         return;
     }
@@ -566,12 +607,12 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
         }
     };
 
-    unsigned best[8];
+    Key best[8];
     int lo[8], len[8], ib0[8];
     unsigned lb[8];            // kPlaneStageMajor: len and lo + ib0 in one register
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-        best[j] = 0xffffffffu;
+        best[j] = KNONE;
         lo[j] = len[j] = ib0[j] = 0;
     }
     // line offsets along each line's own axes (see line_interval)
@@ -737,7 +778,7 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
                     line_interval(po[j], pa[j], pn[j], high[j] == cm, neg[j], d_out, lo[j],
                                   len[j], ib0[j]);
 #pragma unroll
-                for (int j = 0; j < 8; j++)   // len | first candidate index << 16 (len, index < 4096)
+                for (int j = 0; j < 8; j++)   // len | first candidate index << 16 (both < 65536)
                     lb[j] = (unsigned)len[j] | ((unsigned)(lo[j] + ib0[j]) << 16);
                 for (int wc = wlo >> 5; wc <= (whi >> 5); wc++) {
                     unsigned m =
@@ -778,9 +819,10 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
                                     const unsigned sad = V[j] - Pa[j];
                                     const unsigned tt = (unsigned)(d_in - lo[j0 + j]);
                                     const unsigned x = lb[j0 + j];
-                                    const unsigned key = (sad << 12) | (tt + (x >> 16));
+                                    const Key key = WIDE ? ((Key)sad << 32) | (Key)(tt + (x >> 16))
+                                                         : (Key)((sad << 12) | (tt + (x >> 16)));
                                     const bool on = tt < (x & 0xffffu);
-                                    best[j0 + j] = min(best[j0 + j], on ? key : 0xffffffffu);
+                                    best[j0 + j] = min(best[j0 + j], on ? key : KNONE);
                                 }
                             }
                         } else {
@@ -792,7 +834,8 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
                             const unsigned hi =
                                 (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)V);
                             const unsigned sad = hi - Pa + csA[j];
-                            const unsigned key = (sad << 12) | (unsigned)(d_in + ib0[j]);
+                            const Key key = WIDE ? ((Key)sad << 32) | (Key)(unsigned)(d_in + ib0[j])
+                                                 : (Key)((sad << 12) | (unsigned)(d_in + ib0[j]));
                             const bool on = (unsigned)(d_in - lo[j]) < (unsigned)len[j];
                             best[j] = on ? min(best[j], key) : best[j];
                         }
@@ -806,7 +849,7 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     if (keys) {
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-            if ((pn[j] & 0xffff) == 0 || best[j] == 0xffffffffu) continue;
+            if ((pn[j] & 0xffff) == 0 || best[j] == KNONE) continue;
             atomicMin(&keys[(size_t)(ty0 + r0 + j) * W + tx0 + lane], best[j]);
         }
         return;
@@ -818,7 +861,8 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
         const size_t p = (size_t)y * W + x;
         const int4 e = ends[p];
         int cx, cy;
-        line_point(make_line(e.x, e.y, e.z, e.w), (int)(best[j] & 0xfffu), cx, cy);
+        line_point(make_line(e.x, e.y, e.z, e.w), WIDE ? (int)(unsigned)best[j] : (int)(best[j] & 0xfffu),
+                   cx, cy);
         const double dx = (double)(cx - x), dy = (double)(cy - y);
         const int dn = (int)__builtin_sqrt(dx * dx + dy * dy);       // :89
         disp_u8[p] = (uint8_t)dn;
@@ -830,23 +874,41 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
 // The split plane loop's keys -> the reference's outputs: candidate i of the
 // pixel's line, (uchar)(int)sqrt(dx^2 + dy^2) (CameraStereoVision.cpp:85-89).
 // Pixels without a key (not matched) keep what the maps held.
+template <class Key>
 __global__ void ref_finalize_kernel(int W, int H, const int4* __restrict__ ends,
-                                    const unsigned* __restrict__ keys,
+                                    const Key* __restrict__ keys,
                                     uint8_t* __restrict__ disp_u8, uint16_t* __restrict__ disp_u16,
                                     uint8_t* __restrict__ valid_out) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     if (x >= W) return;
     const size_t p = (size_t)y * W + x;
-    const unsigned key = keys[p];
-    if (key == 0xffffffffu) return;
+    const Key key = keys[p];
+    if (key == (Key)~(Key)0) return;
     const int4 e = ends[p];
     int cx, cy;
-    line_point(make_line(e.x, e.y, e.z, e.w), (int)(key & 0xfffu), cx, cy);
+    line_point(make_line(e.x, e.y, e.z, e.w),
+               sizeof(Key) == 8 ? (int)(unsigned)key : (int)((unsigned)key & 0xfffu), cx, cy);
     const double dx = (double)(cx - x), dy = (double)(cy - y);
     const int dn = (int)__builtin_sqrt(dx * dx + dy * dy);       // :89
     disp_u8[p] = (uint8_t)dn;
     if (disp_u16) disp_u16[p] = (uint16_t)dn;
     if (valid_out) valid_out[p] = 1;
+}
+
+// k > 32: one wave per reference pixel over its Bresenham candidates (the
+// 2k-byte rows through sad_span; the per-pixel first minimum is a u64
+// (SAD << 32 | i) wave minimum, so neither k nor the frame size is bounded by
+// a key field).  Four pixels per 256-thread workgroup.
+__global__ __launch_bounds__(256) void ref_pixel_kernel(
+    const uint8_t* __restrict__ ref, const uint8_t* __restrict__ other, int W, int H, size_t pitch,
+    const uint8_t* __restrict__ mask, const int4* __restrict__ ends,
+    const uint8_t* __restrict__ valid_in, int k, uint8_t* __restrict__ disp_u8,
+    uint16_t* __restrict__ disp_u16, uint8_t* __restrict__ valid_out) {
+    const int x = k + (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), y = k + (int)blockIdx.y;
+    if (x >= W - k || y >= H - k) return;                       // wave-uniform
+    const size_t p = (size_t)y * W + x;
+    if (!valid_in[p] || (mask && mask[p] == 0)) return;
+    match_pixel_wave<0>(ref, other, W, pitch, x, y, ends[p], k, disp_u8, disp_u16, valid_out);
 }
 
 __global__ void disp_to_depth_kernel(const uint8_t* __restrict__ disp, int n, double num,
@@ -892,31 +954,45 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
     ScopedKernelTimer t(c, "ref_match");
     const long long npx = (long long)(W - 2 * k) * (H - 2 * k);
     if (npx <= 0) return hipSuccess;
-    // offset-plane algorithm for every k (sva_api checks 1 <= k <= 32)
+    if (k > PT_MAXK) {
+        // windows wider than the plane kernel's region (63 + 2k <= 127
+        // columns): one wave per pixel, first minimum in a u64 wave key
+        const dim3 grid((unsigned)((W - 2 * k + 3) / 4), (unsigned)(H - 2 * k));
+        hipLaunchKernelGGL(ref_pixel_kernel, grid, dim3(256), 0, c.stream, ref, other, W, H, pitch,
+                           mask, (const int4*)ends, valid_in, k, disp_u8, disp_u16, valid_out);
+        return hipGetLastError();
+    }
+    // offset-plane algorithm for k = 1..32
     const int gx = (W - 2 * k + 63) / 64, gy = (H - 2 * k + P3_ROWS - 1) / P3_ROWS;
     const long long tiles = (long long)gx * gy;
     int nsh = plane_shares(tiles, c.cu_count);
-    // test hook: SVA_PLANE_SPLIT=n splits every tile into n shares (1..16),
-    // so the parity tests cover every share count at every size
-    if (const char* e = std::getenv("SVA_PLANE_SPLIT")) {
-        const int n = std::atoi(e);
-        if (n >= 1 && n <= 16) nsh = n;
-    }
+    // SVA_DEBUG_PLANE_SPLIT (sva_set_debug): every tile in n shares, so the
+    // parity tests cover every share count at every size
+    if (c.dbg_plane_split >= 1 && c.dbg_plane_split <= 16) nsh = c.dbg_plane_split;
     const bool split = nsh > 1;
-    unsigned* keys = nullptr;
+    // a line holds at most max(W, H) - 2k + 1 candidates: 4096 or more do not
+    // fit the u32 key's 12-bit index field
+    const bool wide = W >= 4096 || H >= 4096;
+    const size_t kb = wide ? sizeof(unsigned long long) : sizeof(unsigned);
+    void* keys = nullptr;
     if (split) {
-        hipError_t e = c.ref_keys.ensure((size_t)W * H * sizeof(unsigned));
+        hipError_t e = c.ref_keys.ensure((size_t)W * H * kb);
         if (e != hipSuccess) return e;
-        keys = (unsigned*)c.ref_keys.ptr;
-        e = hipMemsetAsync(keys, 0xff, (size_t)W * H * sizeof(unsigned), c.stream);
+        keys = c.ref_keys.ptr;
+        e = hipMemsetAsync(keys, 0xff, (size_t)W * H * kb, c.stream);
         if (e != hipSuccess) return e;
     }
     const dim3 pg3((unsigned)nsh, (unsigned)gx, (unsigned)gy);
-#define SVA_PLANE3_CASE(K_)                                                                    \
-    case K_:                                                                                   \
-        hipLaunchKernelGGL(ref_plane3_kernel<K_>, pg3, dim3(256), 0, c.stream, ref, other, W, H, \
-                           pitch, mask, (const int4*)ends, valid_in, disp_u8, disp_u16,         \
-                           valid_out, keys);                                                   \
+#define SVA_PLANE3_CASE(K_)                                                                        \
+    case K_:                                                                                       \
+        if (wide)                                                                                  \
+            hipLaunchKernelGGL((ref_plane3_kernel<K_, true>), pg3, dim3(256), 0, c.stream, ref,    \
+                               other, W, H, pitch, mask, (const int4*)ends, valid_in, disp_u8,     \
+                               disp_u16, valid_out, keys);                                         \
+        else                                                                                       \
+            hipLaunchKernelGGL((ref_plane3_kernel<K_, false>), pg3, dim3(256), 0, c.stream, ref,   \
+                               other, W, H, pitch, mask, (const int4*)ends, valid_in, disp_u8,     \
+                               disp_u16, valid_out, keys);                                         \
         break;
     switch (k) {
         SVA_PLANE3_CASE(1) SVA_PLANE3_CASE(2) SVA_PLANE3_CASE(3) SVA_PLANE3_CASE(4)
@@ -930,10 +1006,15 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
         default: return hipErrorInvalidValue;
     }
 #undef SVA_PLANE3_CASE
-    if (split)
-        hipLaunchKernelGGL(ref_finalize_kernel, dim3((unsigned)((W + 255) / 256), (unsigned)H),
-                           dim3(256), 0, c.stream, W, H, (const int4*)ends, keys, disp_u8,
-                           disp_u16, valid_out);
+    if (split && wide)
+        hipLaunchKernelGGL(ref_finalize_kernel<unsigned long long>,
+                           dim3((unsigned)((W + 255) / 256), (unsigned)H), dim3(256), 0, c.stream, W,
+                           H, (const int4*)ends, (const unsigned long long*)keys, disp_u8, disp_u16,
+                           valid_out);
+    else if (split)
+        hipLaunchKernelGGL(ref_finalize_kernel<unsigned>, dim3((unsigned)((W + 255) / 256), (unsigned)H),
+                           dim3(256), 0, c.stream, W, H, (const int4*)ends, (const unsigned*)keys,
+                           disp_u8, disp_u16, valid_out);
     return hipGetLastError();
 }
 

@@ -340,13 +340,18 @@ int run_sgm_batch(Ctx* c, const sva_pair_d* jobs, int n, int W, int H, size_t pi
     }
     SVA_HIP(c, c->census_side.ensure(np * 16 * (size_t)std::max(ns, 1)), "census workspace");
     const hipStream_t own = c->stream;
+    // fault injection (SVA_DEBUG_FAIL_COST_AT): this call's n-th cost launch fails
+    const int fail_at = c->dbg_fail_cost_at;
+    c->dbg_fail_cost_at = 0;
     int st = SVA_OK;
     for (int i = 0; i < n && st == SVA_OK; i++) {
         const sva_sgm_params* q = &jobs[i].params;
         uint8_t* Ci = C + (size_t)i * nv;
         if (ns > 1) c->stream = c->side[i % ns];
         hipError_t e;
-        if (q->dir_y == 0 && Dp >= tune::kCensusCostMinD && census_cost_supported(Dp)) {
+        if (i + 1 == fail_at) {
+            e = hipErrorLaunchFailure;
+        } else if (q->dir_y == 0 && Dp >= tune::kCensusCostMinD && census_cost_supported(Dp)) {
             e = launch_census_cost(*c, jobs[i].left, jobs[i].right, W, H, pitch, Dp, q->dmin, q->dir,
                                    Ci, q->D);
         } else if (census_cost2_supported(Dp, q->dir, q->dir_y)) {
@@ -365,31 +370,48 @@ int run_sgm_batch(Ctx* c, const sva_pair_d* jobs, int n, int W, int H, size_t pi
         c->stream = own;
         if (e != hipSuccess) st = hip_fail(c, e, "cost launch");
     }
-    // Aggregation per sub-batch on the context stream, after its costs.  A
-    // failed cost launch still joins every side stream (they stay ordered).
-    for (int j = 0; j < nsub; j++) {
+    // Aggregation per sub-batch on the context stream, after its costs.
+    for (int j = 0; j < nsub && st == SVA_OK; j++) {
         const int i0 = j * sb, m = std::min(sb, n - i0);
+        hipError_t e = hipSuccess;
         if (ns > 1) {
-            for (int s = 0; s < ns && s < n; s++) {
+            for (int s = 0; s < ns && s < n && e == hipSuccess; s++) {
                 // side stream s holds frames of sub-batch j: its event recorded
                 // after the last of them
                 bool has = false;
                 for (int i = i0; i < i0 + m; i++) has = has || i % ns == s;
-                if (!has) continue;
-                SVA_HIP(c, hipStreamWaitEvent(c->stream, c->side_done[(size_t)j * ns + s], 0), "join");
+                if (has) e = hipStreamWaitEvent(c->stream, c->side_done[(size_t)j * ns + s], 0);
             }
         }
-        if (st) continue;
+        if (e != hipSuccess) { st = hip_fail(c, e, "join"); break; }
         uint8_t* L4 = (uint8_t*)c->paths.ptr;
         uint8_t* CK = (uint8_t*)c->ckpt.ptr;
         // horizontal planes of the sub-batch's frames, then their vertical planes
         uint8_t* CKV = CK + tg.hck_bytes * m;
         const uint8_t* Cj = C + (size_t)i0 * nv;
-        SVA_HIP(c, launch_paths(*c, Cj, W, H, Dp, p->P1, p->P2, L4, CK, CKV, m), "paths launch");
-        SVA_HIP(c, launch_wta_hv(*c, Cj, L4, CK, CKV, W, H, Dp, p->P1, p->P2, p->dmin,
-                                 maps + (size_t)i0 * np,
-                                 p->subpixel ? sub + (size_t)i0 * np : nullptr, p->D, m),
-                "wta launch");
+        if ((e = launch_paths(*c, Cj, W, H, Dp, p->P1, p->P2, L4, CK, CKV, m)) != hipSuccess) {
+            st = hip_fail(c, e, "paths launch");
+            break;
+        }
+        if ((e = launch_wta_hv(*c, Cj, L4, CK, CKV, W, H, Dp, p->P1, p->P2, p->dmin,
+                               maps + (size_t)i0 * np, p->subpixel ? sub + (size_t)i0 * np : nullptr,
+                               p->D, m)) != hipSuccess) {
+            st = hip_fail(c, e, "wta launch");
+            break;
+        }
+    }
+    if (st != SVA_OK && ns > 1) {
+        // A failed launch skipped later sub-batches' joins, so the context
+        // stream may not be ordered after cost kernels already queued on the
+        // side streams.  Join every side stream with a fresh record before
+        // returning: the caller may free or reuse the images and the cost
+        // workspace as soon as the context stream has drained.  (side_done[s]
+        // is free for this: nothing later in this call waits on it.)
+        for (int s = 0; s < ns; s++) {
+            if (hipEventRecord(c->side_done[s], c->side[s]) != hipSuccess ||
+                hipStreamWaitEvent(c->stream, c->side_done[s], 0) != hipSuccess)
+                (void)hipStreamSynchronize(c->side[s]);   // last resort: order on the host
+        }
     }
     return st;
 }
@@ -415,12 +437,13 @@ int run_ref_device(Ctx* c, const uint8_t* ref, const uint8_t* other, int W, int 
 }
 
 int check_ref_args(Ctx* c, int W, int H, int k, double t_near, double t_far) {
-    if (k < 1 || k > 32) return fail(c, SVA_ERR_UNSUPPORTED, "kernel half-size k must be 1..32");
-    if (2 * k >= W || 2 * k >= H) return fail(c, SVA_ERR_INVALID_ARG, "image smaller than window");
+    if (k < 1) return fail(c, SVA_ERR_INVALID_ARG, "kernel half-size k must be >= 1");
+    if (2LL * k >= W || 2LL * k >= H) return fail(c, SVA_ERR_INVALID_ARG, "image smaller than window");
     if (!(t_near > 0.0) || !(t_far > 0.0))
         return fail(c, SVA_ERR_INVALID_ARG, "ray parameters must be positive");
-    if (W > 4095 || H > 4095)
-        return fail(c, SVA_ERR_UNSUPPORTED, "Mode R supports W, H < 4096");
+    // the plane kernel packs line geometry in 16-bit fields (refpath.hip)
+    if (W > 32767 || H > 32767)
+        return fail(c, SVA_ERR_UNSUPPORTED, "Mode R supports W, H <= 32767");
     return SVA_OK;
 }
 
@@ -623,6 +646,45 @@ int sva_reset_timing(void* ctx) {
     c->timer.totals.clear();
     if (e != hipSuccess) return hip_fail(c, e, "timer resolve");
     return SVA_OK;
+}
+
+int sva_set_debug(void* ctx, int key, int64_t value) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    switch (key) {
+        case SVA_DEBUG_PLANE_SPLIT:
+            if (value < 0 || value > 16) return fail(c, SVA_ERR_INVALID_ARG, "plane split must be 0..16");
+            c->dbg_plane_split = (int)value;
+            return SVA_OK;
+        case SVA_DEBUG_FAIL_COST_AT:
+            if (value < 0 || value > (1 << 30)) return fail(c, SVA_ERR_INVALID_ARG, "bad frame index");
+            c->dbg_fail_cost_at = (int)value;
+            return SVA_OK;
+        default:
+            return fail(c, SVA_ERR_INVALID_ARG, "unknown or read-only debug key");
+    }
+}
+
+int sva_get_debug(void* ctx, int key, int64_t* value) {
+    Ctx* c = as_ctx(ctx);
+    SVA_CHECK_CTX(c);
+    if (!value) return fail(c, SVA_ERR_INVALID_ARG, "null value");
+    switch (key) {
+        case SVA_DEBUG_PLANE_SPLIT: *value = c->dbg_plane_split; return SVA_OK;
+        case SVA_DEBUG_FAIL_COST_AT: *value = c->dbg_fail_cost_at; return SVA_OK;
+        case SVA_DEBUG_SIDE_IDLE: {
+            bool idle = true;
+            for (hipStream_t s : c->side) {
+                const hipError_t e = hipStreamQuery(s);
+                if (e == hipErrorNotReady) idle = false;
+                else if (e != hipSuccess) return hip_fail(c, e, "side stream query");
+            }
+            *value = idle ? 1 : 0;
+            return SVA_OK;
+        }
+        default:
+            return fail(c, SVA_ERR_INVALID_ARG, "unknown debug key");
+    }
 }
 
 int sva_kernel_time(void* ctx, const char* name, double* total_ms, int64_t* count) {

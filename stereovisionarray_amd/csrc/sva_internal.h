@@ -75,6 +75,11 @@ struct Ctx {
     std::vector<hipEvent_t> side_done;
     hipEvent_t fork = nullptr;
     DevBuf census_side;
+    // sva_set_debug switches (include/sva.h SVA_DEBUG_*): Mode R shares per
+    // tile forced (0 = automatic), and the batch route's injected cost-launch
+    // failure (1-based frame of the next call, 0 = off)
+    int dbg_plane_split = 0;
+    int dbg_fail_cost_at = 0;
 };
 
 // Which launches a timing mode records: SVA_TIMING_ALL every one,

@@ -42,7 +42,7 @@ def test_defaults_and_strings(sva):
     p = sva.default_params()
     assert (p.D, p.dmin, p.dir, p.dir_y, p.P1, p.P2, p.subpixel, p.lr_check, p.invalid) == \
         (128, 0, -1, 0, 10, 120, 0, 0, 0xFFFF)
-    assert sva.lib.sva_abi_version() == 5 == sva.ABI_VERSION
+    assert sva.lib.sva_abi_version() == 6 == sva.ABI_VERSION
     assert sva.lib.sva_status_string(sva.SVA_ERR_NO_DEVICE) == b"no usable HIP device"
 
 

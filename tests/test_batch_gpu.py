@@ -144,3 +144,50 @@ def test_batch_back_to_back_calls(ctx, sva, torch_dev):
             ctx.synchronize()
             assert np.array_equal(got[i], one.cpu().numpy()), i
             assert np.array_equal(gsub[i].view(np.uint32), one_sub.cpu().numpy().view(np.uint32)), i
+
+
+def test_batch_failed_cost_launch_joins_side_streams(ctx, sva, torch_dev):
+    """a cost launch that fails mid-batch must still leave the
+    context stream ordered after every side-stream kernel already queued, so
+    the caller may reuse the images and the cost workspace once the context
+    stream has drained.  SVA_DEBUG_FAIL_COST_AT fails frame 7 of 9 (frames
+    1-6 are queued on the three side streams, big enough to still be running
+    when the call returns); after sva_synchronize of the context stream alone,
+    every side stream must be idle.  The context then keeps working."""
+    H, W, D = 1080, 1920, 128
+    fr = frames(H, W, D, 9, seed=91)
+    dl = [torch.from_numpy(L).to(torch_dev) for L, _, _, _ in fr]
+    dr = [torch.from_numpy(R).to(torch_dev) for _, R, _, _ in fr]
+    pairs = [(dl[i].data_ptr(), dr[i].data_ptr(),
+              sva.default_params(D=D, dir=fr[i][2], dir_y=fr[i][3], subpixel=1))
+             for i in range(len(fr))]
+    maps = torch.zeros((len(fr), H, W), dtype=torch.int16, device=torch_dev)
+    sub = torch.zeros((len(fr), H, W), dtype=torch.float32, device=torch_dev)
+    torch.cuda.synchronize()
+    ctx.set_debug(sva.SVA_DEBUG_FAIL_COST_AT, 7)
+    with pytest.raises(sva.SvaError) as e:
+        ctx.disparity_sgm_batch_d(pairs, W, H, W, maps.data_ptr(), sub.data_ptr())
+    assert e.value.status == sva.SVA_ERR_DEVICE
+    assert ctx.get_debug(sva.SVA_DEBUG_FAIL_COST_AT) == 0      # one-shot
+    ctx.synchronize()                                           # the context stream only
+    assert ctx.get_debug(sva.SVA_DEBUG_SIDE_IDLE) == 1
+    # the same context and workspaces afterwards: frames 1..3 through the batch
+    # route equal the single-frame route
+    got, gsub, ref_m, ref_s = run_batch(ctx, sva, torch_dev, fr[:3], D)
+    for i in range(3):
+        assert np.array_equal(got[i].view(np.uint16), ref_m[i].view(np.uint16)), i
+        assert np.array_equal(gsub[i].view(np.uint32), ref_s[i].view(np.uint32)), i
+
+
+def test_debug_switch_keys(ctx, sva):
+    """sva_set_debug / sva_get_debug: range checks, read-only and unknown keys."""
+    with pytest.raises(sva.SvaError):
+        ctx.set_debug(sva.SVA_DEBUG_PLANE_SPLIT, 17)
+    with pytest.raises(sva.SvaError):
+        ctx.set_debug(sva.SVA_DEBUG_SIDE_IDLE, 1)
+    with pytest.raises(sva.SvaError):
+        ctx.get_debug(99)
+    ctx.set_debug(sva.SVA_DEBUG_PLANE_SPLIT, 3)
+    assert ctx.get_debug(sva.SVA_DEBUG_PLANE_SPLIT) == 3
+    ctx.set_debug(sva.SVA_DEBUG_PLANE_SPLIT, 0)
+    assert ctx.get_debug(sva.SVA_DEBUG_PLANE_SPLIT) == 0

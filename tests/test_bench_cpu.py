@@ -118,13 +118,18 @@ def fake_mode_r_pass(seen, ran=None):
 
 
 def test_mode_r_valu_roofline(bench, monkeypatch):
-    """VERDICT r03 next #5: SQ_INSTS_VALU x 4 / (1024 SIMDs x 2.4 GHz x kernel time)."""
+    """the VALU peak is the SIMD-32 issue rate,
+    one wave64 instruction per 2 cycles per SIMD (MI355X_MICROARCH.md :53-54):
+    SQ_INSTS_VALU / (kernel time x 1,024 x 2.4 GHz / 2) -- not the 4 cycles
+    one wave alone sustains, which rounds 3-5 used."""
     seen = {}
     monkeypatch.setattr(bench, "_pmc_pass", fake_mode_r_pass(seen))
     rf = bench.mode_r_roofline({"ref_match_kernel_ms": 0.8, "W": 1920, "H": 1080})
-    assert seen["counter"] == "SQ_INSTS_VALU GRBM_GUI_ACTIVE"
+    assert seen["counter"] == bench.SQ_VALU_COUNTERS
+    assert "SQ_WAIT_INST_ANY" in seen["counter"] and "SQ_ACTIVE_INST_VALU" in seen["counter"]
     assert seen["child"] == ["--mode-r-only", "--mode-r-size", "1920x1080"]
-    assert abs(rf["frac"] - 300e6 * 4 / (1024 * 2.4e9 * 0.8e-3)) < 1e-4
+    assert bench.VALU_ISSUE_CYCLES == 2.0 and abs(bench.VALU_PEAK_PER_S - 1.2288e12) < 1e3
+    assert abs(rf["frac"] - 300e6 * 2 / (1024 * 2.4e9 * 0.8e-3)) < 1e-4
     assert rf["bound"] == "valu" and rf["sq_insts_valu"] == 300000000
     assert rf["frame"] == "1920x1080"
     with pytest.raises(RuntimeError):
@@ -216,3 +221,43 @@ def test_batch_groups_and_frames_per_launch(bench):
     assert bench.batch_frames_per_launch(256) == 4.0
     assert bench.batch_frames_per_launch(11) == 11 / 3       # 8 -> 4 + 4, 3
     assert bench.batch_frames_per_launch(8, 3) == 8 / 3      # 2, 3, 3 frames: one launch each
+
+
+def test_valu_roofline_shares_and_clock(bench):
+    """valu_roofline: issue fraction at the peak clock, at the kernel's own
+    active cycles (GRBM_GUI_ACTIVE summed over 8 XCDs), and the SQ_WAVE_CYCLES
+    shares spent issuing VALU and waiting."""
+    c = {"SQ_INSTS_VALU": 120e6, "SQ_ACTIVE_INST_VALU": 120e6, "SQ_WAIT_INST_ANY": 90e6,
+         "SQ_WAIT_ANY": 150e6, "SQ_WAVE_CYCLES": 600e6, "GRBM_GUI_ACTIVE": 8 * 500e3,
+         "_dur_ns": 250e3}
+    rf = bench.valu_roofline("wta_hv", c, 0.25, "wta_hv_kernel")
+    assert abs(rf["frac"] - 120e6 / (0.25e-3 * 1.2288e12)) < 1e-4
+    assert abs(rf["frac_at_clock"] - 2 * 120e6 / (1024 * 500e3)) < 1e-4
+    assert rf["clock_ghz"] == 2.0
+    assert rf["active_valu_share"] == 0.2 and rf["wait_inst_any_share"] == 0.15
+    assert rf["wait_any_share"] == 0.25
+    with pytest.raises(RuntimeError):
+        bench.valu_roofline("wta_hv", {}, 0.25, "wta_hv_kernel")
+
+
+def test_ea_figures(bench):
+    """roofline.engine: engine clock from GRBM_GUI_ACTIVE
+    over the pass's kernel duration, EA read bytes at 128 B per request
+    (gfx950), write bytes from the 64-B and 32-B request counts."""
+    c = {"TCC_EA0_RDREQ_sum": 1e6, "TCC_EA0_WRREQ_sum": 3e6, "TCC_EA0_WRREQ_64B_sum": 2e6,
+         "GRBM_GUI_ACTIVE": 8 * 2.1e6, "_dur_ns": 1e6}
+    e = bench.ea_figures(c, 1.0)
+    assert e["clock_ghz"] == 2.1
+    assert e["ea_read_bytes"] == 128e6 and e["ea_write_bytes"] == 2e6 * 64 + 1e6 * 32
+    assert e["ea_bytes"] == e["ea_read_bytes"] + e["ea_write_bytes"]
+    assert e["ea_gbs_at_event_time"] == round(e["ea_bytes"] / 1e-3 / 1e9, 1)
+
+
+def test_engine_counters_skipped_off_the_live_route(bench, monkeypatch):
+    called = []
+    monkeypatch.setattr(bench, "engine_counters", lambda a: called.append(1) or ({}, {}))
+    out = line(bench)
+    a = args("committed")
+    bench.attach_engine(a, out, {}, 1)
+    bench.attach_engine(args("live"), out, {}, 2)
+    assert not called and "valu_roofline" not in out

@@ -262,14 +262,15 @@ def test_ref_path_4k_row_sampled(ctx, sva, oracle, pair):
 
 # The split plane loop (refpath.hip: a tile's inner offsets over several
 # workgroups, first-minimum keys meeting by atomicMin, ref_finalize_kernel):
-# the host picks it for tile grids that fill the chip poorly (the reference's
-# half-size frames); SVA_PLANE_SPLIT forces a share count so that every size
-# and the per-pixel fallback run through it too.
+# the host splits every tile over 3-6 shares; SVA_DEBUG_PLANE_SPLIT
+# (sva_set_debug) forces a share count so that every size and the per-pixel
+# fallback run through it too.  The switch is reset afterwards.
 @pytest.fixture()
-def plane_split(monkeypatch):
+def plane_split(ctx, sva):
     def set_(n):
-        monkeypatch.setenv("SVA_PLANE_SPLIT", str(n))
-    return set_
+        ctx.set_debug(sva.SVA_DEBUG_PLANE_SPLIT, n)
+    yield set_
+    ctx.set_debug(sva.SVA_DEBUG_PLANE_SPLIT, 0)
 
 
 @pytest.mark.parametrize("shares", [1, 2, 3, 7])
@@ -319,3 +320,76 @@ def test_ref_path_split_fallback_diagonal_jump(ctx, sva, oracle, plane_split, sh
 def test_ref_path_split_1080p_row_sampled(ctx, sva, oracle, plane_split, pair):
     plane_split(3)
     test_ref_path_1080p_row_sampled(ctx, sva, oracle, pair)
+
+
+# VERDICT r05 missing #3: the reference bounds neither k nor the frame
+# (CameraStereoVision.cpp:44-51, :76-85).  k > 32 runs ref_pixel_kernel (one
+# wave per pixel, 2k-byte rows in 64-byte chunks plus a tail); W or H >= 4096
+# runs the WIDE plane kernel, whose first-minimum keys are u64 (SAD << 32 | i).
+@pytest.mark.parametrize("k", [33, 34, 40, 64])
+@pytest.mark.parametrize("pair", [(12, 11), (12, 7), (12, 18)])
+def test_ref_path_k_above_32(ctx, sva, oracle, k, pair):
+    W, H = 640, 480
+    cr, co, ocr, oco = cams_for(sva, oracle, W, *pair)
+    a = synth.texture(H, W, 40 + k)
+    gx, gy = pair[1] % 5 - 2, pair[1] // 5 - 2
+    b = np.roll(np.roll(a, -60 * gy, axis=0), -60 * gx, axis=1)
+    mask = np.zeros((H, W), np.uint8)          # a band of rows keeps the oracle in seconds
+    mask[H // 2 - 4: H // 2 + 4, :] = 1
+    mask[k + 1, :] = 1                         # and the first rows the window allows
+    mask[H - k - 2, ::7] = 1
+    d8_0 = np.full((H, W), 201, np.uint8)
+    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k, mask=mask, disp_u8=d8_0.copy())
+    o8, o16, ov, n = oracle.ref_pair(a, b, ocr, oco, k=k, mask=mask, disp_u8=d8_0.copy())
+    assert n > 0 and ov.sum() > 0
+    assert np.array_equal(valid, ov) and np.array_equal(d16, o16) and np.array_equal(d8, o8)
+
+
+@pytest.mark.parametrize("shares", [0, 1, 3])
+def test_ref_path_wide_frame_4160(ctx, sva, oracle, plane_split, shares):
+    """A 4160 x 96 frame (pair 12 -> 11, k = 20): past the u32 key's 4096
+    columns, through the WIDE plane kernel unsplit (1), split (3) and with the
+    automatic share count (0)."""
+    plane_split(shares)
+    W, H, k = 4160, 96, 20
+    cr, co, ocr, oco = cams_for(sva, oracle, W, 12, 11)
+    a = synth.texture(H, W, 17)
+    b = np.roll(a, 300, axis=1)
+    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k)
+    o8, o16, ov, n = oracle.ref_pair(a, b, ocr, oco, k=k)
+    assert n > 0 and ov.sum() > 1000
+    assert np.array_equal(valid, ov) and np.array_equal(d16, o16) and np.array_equal(d8, o8)
+
+
+@pytest.mark.parametrize("shares", [1, 3])
+def test_ref_path_wide_keys_index_past_4095(ctx, sva, oracle, plane_split, shares):
+    """Lines of more than 4096 candidates whose first minimum sits at index
+    > 4095: a 4600 x 64 frame with t_near = 0.071 (a ~4,340-point line per
+    pixel near the right border) and the other image shifted 300 px, so the
+    exact match is at candidate ~4,200.  The u32 key's 12-bit index would
+    alias it; the WIDE key must not."""
+    plane_split(shares)
+    W, H, k = 4600, 64, 4
+    cr, co, ocr, oco = cams_for(sva, oracle, W, 12, 11)
+    a = synth.texture(H, W, 23)
+    b = np.roll(a, 300, axis=1)
+    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k, t_near=0.071, t_far=2.0)
+    o8, o16, ov, n = oracle.ref_pair(a, b, ocr, oco, k=k, t_near=0.071, t_far=2.0)
+    assert ov.sum() > 100 and n > 4096 * ov.sum() // 2
+    assert np.array_equal(valid, ov) and np.array_equal(d16, o16) and np.array_equal(d8, o8)
+    assert (o16[ov > 0] > 250).mean() > 0.5     # matches at the 300 px shift, not aliased
+
+
+def test_ref_path_limits(ctx, sva):
+    """What Mode R still refuses: k < 1, a window not inside the image
+    (2k >= W or H, the reference's own loop bounds), W or H > 32767."""
+    W, H = 64, 48
+    a = np.zeros((H, W), np.uint8)
+    cr = sva.Camera.make(0.05, (0.0, 0.0, 0.0), 0.036 / W)
+    co = sva.Camera.make(0.05, (-0.05, 0.0, 0.0), 0.036 / W)
+    for k, status in ((0, sva.SVA_ERR_INVALID_ARG), (24, sva.SVA_ERR_INVALID_ARG)):
+        with pytest.raises(sva.SvaError) as e:
+            ctx.disparity_ref(a, a, cr, co, k=k)
+        assert e.value.status == status
+    d8, _, v = ctx.disparity_ref(a, a, cr, co, k=23)        # 2k = 46 < 48: accepted
+    assert d8.shape == (H, W)
