@@ -423,7 +423,12 @@ VALU_PEAK_SOURCE = ("1,024 SIMD-32 units x 2.4 GHz / 2 cycles per wave64 VALU in
 # wta_hv_kernel<8,3,false> and of ref_plane3_kernel<20>'s per-plane body,
 # tools/isa_mix.py), best of 1/2/4/8 waves per SIMD, chip-wide wave-instructions
 # per second from the kernel's hipEvent time (profiles/r06_v1/microbench_valu.txt).
-VALU_MIX_PEAK_PER_S = {}
+# Measured: 64-bit-encoded VALU (VOP3 / VOP3P / DPP: v_perm, v_add3, v_pk_*,
+# v_sad_u8, DPP min/add) issue at about half the SIMD-32 rate on gfx950
+# (0.47 of 1.229e12 at 8 waves/SIMD), 32-bit VOP2 at 0.84 (v_add_u32), and
+# these kernels are ~90 % the former.  sgm_paths runs the same recurrence
+# step as wta_hv, so it is graded on the wta_hv mix.
+VALU_MIX_PEAK_PER_S = {"wta_hv": 5.931e11, "sgm_paths": 5.931e11, "ref_match": 6.348e11}
 VALU_MIX_SOURCE = "tools/microbench_valu.hip mix kinds, profiles/r06_v1/microbench_valu.txt"
 SQ_VALU_COUNTERS = ("SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES "
                     "SQ_BUSY_CYCLES GRBM_GUI_ACTIVE")

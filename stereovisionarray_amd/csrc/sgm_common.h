@@ -214,10 +214,21 @@ __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigne
     u16x2 t[NP];
 #pragma unroll
     for (int j = 0; j < NP; j++) t[j] = vmin2(as_v2(M[j]), as_v2(j < NP - 1 ? M[j + 1] : Qlast));
+    unsigned tp[NP];
+    if constexpr (tune::kStepAddU32 != 0) {
+        // + P1 in both halves as ONE 32-bit add (VOP2, full issue rate; the
+        // packed v_pk_add_u16 is a 64-bit VOP3P encoding that issues at half
+        // rate, profiles/r06_v1/microbench_valu.txt): t <= 448 + 193 per half
+        // (INF never reaches t, see min3_u16x2), so the low half never carries
+        const unsigned P1x2 = P1 * 0x10001u;
 #pragma unroll
-    for (int j = 0; j < NP; j++) t[j] = t[j] + splat2(P1);
+        for (int j = 0; j < NP; j++) tp[j] = as_u32(t[j]) + P1x2;
+    } else {
 #pragma unroll
-    for (int j = 0; j < NP; j++) A[j] = add3(min3_u16x2(as_u32(t[j]), A[j], mP2), c[j], K);
+        for (int j = 0; j < NP; j++) tp[j] = as_u32(t[j] + splat2(P1));
+    }
+#pragma unroll
+    for (int j = 0; j < NP; j++) A[j] = add3(min3_u16x2(tp[j], A[j], mP2), c[j], K);
 #pragma unroll
     for (int w = 0; w < NW; w++) ow[w] = pack4(A[2 * w], A[2 * w + 1]);
     m = row_min_u32<PIN>(lane_min_u16<NP>(A));

@@ -96,7 +96,7 @@ __global__ __launch_bounds__(PATH_BLOCK) void sgm_paths_kernel(const uint8_t* __
     const rsrc_t rC = make_rsrc(C, g.vol);
     // the tile pipeline's checkpoint segment (§4.9), rows and columns
     constexpr int SL = DPL <= 8 ? tune::kWtahvTileLog2 : tune::kWtahvTileLog2Wide;
-    constexpr bool DOWN = tune::kTileDiagDown != 0, UP = tune::kTileDiagUp != 0;
+    constexpr bool DOWN = diag_ckpt_down(DPL), UP = diag_ckpt_up(DPL);
     if (r >= 4 && g.ckpt && (ry > 0 ? DOWN : UP)) {
         // tile pipeline, diagonals recomputed per tile: row
         // checkpoints only, in the vertical checkpoint block after the two
@@ -141,7 +141,8 @@ TileGeom tile_geom(int W, int H, int D) {
     t.nsx = (W + seg - 1) >> t.seg_log2;
     t.hck_bytes = 2 * (size_t)H * t.nsx * D;
     t.vck_bytes = 2 * (size_t)t.nty * W * D;
-    const int ndp = (tune::kTileDiagDown ? 2 : 0) + (tune::kTileDiagUp ? 2 : 0);
+    const int dpl = D / 16;
+    const int ndp = (diag_ckpt_down(dpl) ? 2 : 0) + (diag_ckpt_up(dpl) ? 2 : 0);
     t.dck_bytes = (size_t)ndp / 2 * t.vck_bytes;   // one plane per recomputed diagonal
     t.nvol = 4 - ndp;
     return t;

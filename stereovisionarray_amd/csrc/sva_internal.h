@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "sva.h"
+#include "sva_tuning.h"
 
 namespace sva {
 
@@ -178,6 +179,21 @@ struct TileGeom {
     int nvol;                 // diagonal volumes the path kernel writes: 2 (5, 7) or 4
 };
 TileGeom tile_geom(int W, int H, int D);
+// Which diagonal pairs the path kernel leaves as row checkpoints instead of
+// volumes, per lane width DPL = D / 16: all four on the strip route (D <= 128,
+// tune::kStripRoute), else the §4.11 experiment's switches.
+constexpr bool diag_ckpt_down(int dpl) {
+    return (tune::kStripRoute != 0 && dpl <= 8) || tune::kTileDiagDown != 0;
+}
+constexpr bool diag_ckpt_up(int dpl) {
+    return (tune::kStripRoute != 0 && dpl <= 8) || tune::kTileDiagUp != 0;
+}
+// wta_strip.hip -- the strip route's final kernel (all eight directions per
+// tile from the checkpoints of launch_paths at D <= 128, no volume)
+bool wta_strip_supported(int D);
+hipError_t launch_wta_strip(Ctx& c, const uint8_t* C, const uint8_t* CK, const uint8_t* CKV, int W,
+                            int H, int D, int P1, int P2, int dmin, uint16_t* disp, float* sub,
+                            int dreal = 0, int npair = 1);
 bool paths_supported(int D);
 // Native volume width of a frame with D disparities: 64, 128, 192 or 256
 // (the smallest >= D), 0 when D is outside 1..256.

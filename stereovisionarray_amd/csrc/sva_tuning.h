@@ -13,6 +13,10 @@ namespace sva {
 namespace tune {
 
 // ---- sgm_paths.hip / sgm_common.h ------------------------
+// The recurrence step's "+ P1" as one v_add_u32 per pair (1) instead of
+// v_pk_add_u16 (0): VOP2 issues at ~2x the rate of VOP3P on gfx950
+// (profiles/r06_v1/microbench_valu.txt).
+constexpr int kStepAddU32 = 1;
 // Prefetch ring depth in steps, per line kind and disparities per lane
 // (D = 16 * DPL).  Horizontal lines are few (2H) and long (W steps) and run
 // alone once the vertical/diagonal lines drain, so they get the deeper ring.
@@ -75,6 +79,17 @@ constexpr int kStateMinTree = 1;
 // 3.772 / 3.863 / 3.944, 4K D=256 7.570 / 7.394 / 7.697.
 constexpr int kTileDiagDown = 0;
 constexpr int kTileDiagUp = 0;
+// The strip route: at D <= 128 sgm_paths writes
+// row checkpoints for all four diagonals and no volume at all, and
+// wta_strip_kernel recomputes all eight directions per tile, walking strips
+// of tiles so that every diagonal line runs once (no per-tile halo).
+// kStripTileW: tile columns (16 or 32; 32 x 16 lanes = 512 threads);
+// kStripCols: strip length in columns (rounded to whole tiles, evened out).
+constexpr int kStripRoute = 0;
+constexpr int kStripTileW = 16;
+constexpr int kStripCols = 128;
+// minimum waves per SIMD asked of the compiler (launch bounds)
+constexpr int kStripMinWaves = 3;
 // log2 of the tile rows and of the checkpoint segment (tiles are 16 x 2^this).
 constexpr int kWtahvTileLog2 = 3;
 constexpr int kWtahvTileLog2Wide = 3;      // D > 128

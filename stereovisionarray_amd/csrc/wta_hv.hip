@@ -74,7 +74,7 @@ __global__ __launch_bounds__(TB, tune::kWtahvMinWaves) void wta_hv_kernel(const 
     const int tx = (int)(tb % (unsigned)g.ntx);
     const int ty = (int)(tb / (unsigned)g.ntx);
     // diagonals recomputed per tile (§4.11): the down pair (4, 6), the up pair (5, 7)
-    constexpr bool DOWN = tune::kTileDiagDown != 0, UP = tune::kTileDiagUp != 0;
+    constexpr bool DOWN = diag_ckpt_down(DPL), UP = diag_ckpt_up(DPL);
     constexpr int ND = (DOWN ? 2 : 0) + (UP ? 2 : 0);   // recomputed diagonals
     constexpr int NV = 4 - ND;                          // diagonal volumes read
     C += (size_t)f * g.vol;
@@ -470,6 +470,10 @@ bool wta_hv_supported(int D) { return D == 64 || D == 128 || D == 192 || D == 25
 hipError_t launch_wta_hv(Ctx& c, const uint8_t* C, const uint8_t* L4, const uint8_t* CK,
                          const uint8_t* CKV, int W, int H, int D, int P1, int P2, int dmin,
                          uint16_t* disp, float* sub, int dreal, int npair) {
+    // D <= 128 on the strip route: all eight directions recomputed per tile
+    // from checkpoints, no diagonal volume (wta_strip.hip)
+    if (tune::kStripRoute != 0 && wta_strip_supported(D))
+        return launch_wta_strip(c, C, CK, CKV, W, H, D, P1, P2, dmin, disp, sub, dreal, npair);
     DispatchTimer t(c, "wta_hv");
     if (!wta_hv_supported(D)) return hipErrorInvalidValue;
     const TileGeom tg = tile_geom(W, H, D);

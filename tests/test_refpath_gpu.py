@@ -364,20 +364,20 @@ def test_ref_path_wide_frame_4160(ctx, sva, oracle, plane_split, shares):
 @pytest.mark.parametrize("shares", [1, 3])
 def test_ref_path_wide_keys_index_past_4095(ctx, sva, oracle, plane_split, shares):
     """Lines of more than 4096 candidates whose first minimum sits at index
-    > 4095: a 4600 x 64 frame with t_near = 0.071 (a ~4,340-point line per
-    pixel near the right border) and the other image shifted 300 px, so the
-    exact match is at candidate ~4,200.  The u32 key's 12-bit index would
-    alias it; the WIDE key must not."""
+    > 4095: a 4600 x 64 frame, pair 12 -> 11 with t_near = 0.0745, t_far = 2
+    (pixels x <= 45 keep ~4,380-point lines) and the other image rolled by
+    4,300 px, so the exact match is candidate ~4,126.  The u32 key's 12-bit
+    index would alias it; the WIDE key must not."""
     plane_split(shares)
     W, H, k = 4600, 64, 4
     cr, co, ocr, oco = cams_for(sva, oracle, W, 12, 11)
     a = synth.texture(H, W, 23)
-    b = np.roll(a, 300, axis=1)
-    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k, t_near=0.071, t_far=2.0)
-    o8, o16, ov, n = oracle.ref_pair(a, b, ocr, oco, k=k, t_near=0.071, t_far=2.0)
-    assert ov.sum() > 100 and n > 4096 * ov.sum() // 2
+    b = np.roll(a, 4300, axis=1)
+    d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=k, t_near=0.0745, t_far=2.0)
+    o8, o16, ov, n = oracle.ref_pair(a, b, ocr, oco, k=k, t_near=0.0745, t_far=2.0)
+    assert ov.sum() > 1000 and n > 4096 * int(ov.sum())
+    assert (o16[ov > 0] == 4300).mean() > 0.3      # matched at index 4300 - 174 > 4095
     assert np.array_equal(valid, ov) and np.array_equal(d16, o16) and np.array_equal(d8, o8)
-    assert (o16[ov > 0] > 250).mean() > 0.5     # matches at the 300 px shift, not aliased
 
 
 def test_ref_path_limits(ctx, sva):

@@ -1,5 +1,5 @@
 """The frame route's two stages (the tile pipeline)
-through their ABI v5 entry points, against the CPU oracle, bit-exact:
+through their ABI v6 entry points, against the CPU oracle, bit-exact:
 sva_paths_tile_d writes the diagonal volumes and the checkpoints (the
 oracle's L_0 / L_1 at the checkpoint columns, L_2 / L_3 at the checkpoint
 rows, and in a build that recomputes the down diagonals per tile their L_4 /
@@ -58,9 +58,10 @@ def check_stages(oracle, C, dmin, res, P1=10, P2=120):
     diag, hck, vck, disp, sub, lay = res
     seg = lay.seg
     vols = [oracle.path(C, r, P1, P2) for r in range(8)]
-    # volumes: the up diagonals 5, 7 (their down pair is recomputed per tile,
-    # DESIGN.md §4.11), or all four diagonals in a build that writes them
-    vol_dirs = [5, 7] if lay.diag_volumes == 2 else [4, 5, 6, 7]
+    # volumes: all four diagonals (the wta_hv route, D >= 192), none (the
+    # strip route, D <= 128: all eight directions recomputed per tile,
+    # DESIGN.md §4.12), or the up diagonals 5, 7 in the §4.11 experiment build
+    vol_dirs = {4: [4, 5, 6, 7], 2: [5, 7], 0: []}[lay.diag_volumes]
     for slot, r in enumerate(vol_dirs):
         assert np.array_equal(diag[slot], vols[r]), f"direction {r}"
     for s in range(lay.nsx):
@@ -73,9 +74,12 @@ def check_stages(oracle, C, dmin, res, P1=10, P2=120):
             assert np.array_equal(vck[0, s], vols[2][s * seg + seg - 1]), ("v0", s)
         if s > 0:                      # L_3 at the segment's first row
             assert np.array_equal(vck[1, s], vols[3][s * seg]), ("v1", s)
-        if lay.diag_volumes == 2 and s * seg + seg < H:   # L_4, L_6 at the last row
+        if lay.diag_volumes <= 2 and s * seg + seg < H:   # L_4, L_6 at the last row
             assert np.array_equal(vck[2, s], vols[4][s * seg + seg - 1]), ("d4", s)
             assert np.array_equal(vck[3, s], vols[6][s * seg + seg - 1]), ("d6", s)
+        if lay.diag_volumes == 0 and s > 0:                # L_5, L_7 at the first row
+            assert np.array_equal(vck[4, s], vols[5][s * seg]), ("d5", s)
+            assert np.array_equal(vck[5, s], vols[7][s * seg]), ("d7", s)
     S = np.zeros(C.shape, np.uint16)
     for v in vols:
         S += v
@@ -132,6 +136,8 @@ def test_undersized_buffers_refused(ctx, sva, torch_dev):
     p = sva.default_params(D=D)
     full = [lay.cost_bytes, lay.diag_bytes, lay.hckpt_bytes, lay.vckpt_bytes]
     for i in range(4):
+        if full[i] == 0:            # no diagonal volume on the strip route (D <= 128)
+            continue
         sizes = list(full)
         sizes[i] -= 1
         with pytest.raises(sva.SvaError) as e:
