@@ -205,7 +205,17 @@ def mode_r_beside(ctx, W, H, rows=24, k=20, reps=10):
               f"sample of {rows} of the frame's {H} rows (the middle band, masked), "
               f"{ncpu} candidates, {cdt:.2f} s; the rate is per candidate SAD, so it does "
               "not depend on how many rows the sample holds")
+    # pixel-SADs the plane kernel evaluates per candidate
+    # the reference uses (sampled tiles, tools/mode_r_planes.py)
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import mode_r_planes
+        red = mode_r_planes.pair_ratio(W, H, k, 12, 11, mode_r_planes.sample_tiles(W, H, k),
+                                       ends=e, ok=okn)     # the GPU's own endpoints
+    except Exception as e:                      # a report, never the bench's failure
+        red = {"error": str(e)[:120]}
     return {"unit": "Mcandidate-SADs/s", "gpu": round(g, 1), "gpu_ms_per_frame": round(gdt * 1e3, 3),
+            "sad_planes_per_candidate": red,
             "W": W, "H": H,
             "ref_match_kernel_ms": round(km / kn, 4) if kn else None,
             "cpu": round(c, 3), "cores": 1, "kind": "port", "sample": sample,

@@ -402,8 +402,13 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
     // (the arrays above plus 256 B of alignment slack)
     constexpr size_t LDS_BASE = sizeof(RT) + sizeof(bits) + sizeof(OUT) + sizeof(omn) + sizeof(omx) +
                                 sizeof(box) + sizeof(uniq) + sizeof(nuniq);
+    // LDS per CU: 160 KB on gfx950, the only target this file is built for
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "refpath.hip sizes its LDS for gfx950 (160 KB per CU)"
+#endif
+    constexpr size_t LDS_PER_CU = 160 * 1024;
     constexpr bool POLDS = tune::kPlanePoLds != 0 &&
-                           LDS_BASE + 8 * 256 * sizeof(int) + 256 <= 160 * 1024 / tune::kPlaneMinBlocks;
+                           LDS_BASE + 8 * 256 * sizeof(int) + 256 <= LDS_PER_CU / tune::kPlaneMinBlocks;
     __shared__ int po_lds[POLDS ? 8 * 256 : 1];
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -873,7 +878,8 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
 
 // The split plane loop's keys -> the reference's outputs: candidate i of the
 // pixel's line, (uchar)(int)sqrt(dx^2 + dy^2) (CameraStereoVision.cpp:85-89).
-// Pixels without a key (not matched) keep what the maps held.
+// Pixels without a key (not matched) keep what the maps held.  Each key read
+// is put back to all-ones, so the next call needs no memset.
 template <class Key>
 __global__ void ref_finalize_kernel(int W, int H, const int4* __restrict__ ends,
                                     const Key* __restrict__ keys,
@@ -884,6 +890,7 @@ __global__ void ref_finalize_kernel(int W, int H, const int4* __restrict__ ends,
     const size_t p = (size_t)y * W + x;
     const Key key = keys[p];
     if (key == (Key)~(Key)0) return;
+    const_cast<Key*>(keys)[p] = (Key)~(Key)0;
     const int4 e = ends[p];
     int cx, cy;
     line_point(make_line(e.x, e.y, e.z, e.w),
@@ -976,11 +983,22 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
     const size_t kb = wide ? sizeof(unsigned long long) : sizeof(unsigned);
     void* keys = nullptr;
     if (split) {
-        hipError_t e = c.ref_keys.ensure((size_t)W * H * kb);
+        const size_t need = (size_t)W * H * kb;
+        hipError_t e = c.ref_keys.ensure(need);
         if (e != hipSuccess) return e;
         keys = c.ref_keys.ptr;
-        e = hipMemsetAsync(keys, 0xff, (size_t)W * H * kb, c.stream);
-        if (e != hipSuccess) return e;
+        if (c.ref_keys_alloc != c.ref_keys.ptr) {   // a new allocation: nothing known clean
+            c.ref_keys_alloc = c.ref_keys.ptr;
+            c.ref_keys_clean = 0;
+        }
+        if (c.ref_keys_clean < need) {
+            // the only memset: the first call, or a buffer past what earlier
+            // finalize passes restored to all-ones
+            e = hipMemsetAsync(keys, 0xff, need, c.stream);
+            if (e != hipSuccess) return e;
+            c.ref_keys_clean = need;
+        }
+        c.ref_keys_clean = 0;                        // until the finalize below is queued
     }
     const dim3 pg3((unsigned)nsh, (unsigned)gx, (unsigned)gy);
 #define SVA_PLANE3_CASE(K_)                                                                        \
@@ -1015,7 +1033,10 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
         hipLaunchKernelGGL(ref_finalize_kernel<unsigned>, dim3((unsigned)((W + 255) / 256), (unsigned)H),
                            dim3(256), 0, c.stream, W, H, (const int4*)ends, (const unsigned*)keys,
                            disp_u8, disp_u16, valid_out);
-    return hipGetLastError();
+    const hipError_t err = hipGetLastError();
+    // the finalize pass restores every key of the W x H region to all-ones
+    if (split && err == hipSuccess) c.ref_keys_clean = (size_t)W * H * (wide ? 8 : 4);
+    return err;
 }
 
 hipError_t launch_disp_to_depth(Ctx& c, const uint8_t* disp, int n, double cam_distance,

@@ -64,8 +64,13 @@ struct Ctx {
     DevBuf in_a, in_b, in_mask, out_a, out_b, out_c;
     // refinement / 3-D workspace (refine.hip)
     DevBuf in_c, shifted, keys, counts, total;
-    // Mode R's split plane loop: one first-minimum key per pixel (refpath.hip)
+    // Mode R's split plane loop: one first-minimum key per pixel (refpath.hip).
+    // ref_finalize_kernel puts every key it reads back to all-ones, so after
+    // the first call only a grown buffer needs the memset: ref_keys_clean =
+    // leading bytes known to be all-ones (of allocation ref_keys_alloc)
     DevBuf ref_keys;
+    size_t ref_keys_clean = 0;
+    const void* ref_keys_alloc = nullptr;
     int cu_count = 256;
     // sva_batch_sgm's per-context pipeline (copy streams, events, pinned and
     // device staging), created on first use and kept for later calls
@@ -181,7 +186,7 @@ struct TileGeom {
 TileGeom tile_geom(int W, int H, int D);
 // Which diagonal pairs the path kernel leaves as row checkpoints instead of
 // volumes, per lane width DPL = D / 16: all four on the strip route (D <= 128,
-// tune::kStripRoute, DESIGN.md §4.12), else the §4.11 experiment's switches.
+// tune::kStripRoute, DESIGN.md §4.13), else the §4.11 experiment's switches.
 constexpr bool diag_ckpt_down(int dpl) {
     return (tune::kStripRoute != 0 && dpl <= 8) || tune::kTileDiagDown != 0;
 }

@@ -79,12 +79,17 @@ constexpr int kStateMinTree = 1;
 // 3.772 / 3.863 / 3.944, 4K D=256 7.570 / 7.394 / 7.697.
 constexpr int kTileDiagDown = 0;
 constexpr int kTileDiagUp = 0;
-// The strip route (DESIGN.md §4.12, round 6): at D <= 128 sgm_paths writes
+// The strip route (DESIGN.md §4.13, round 6): at D <= 128 sgm_paths writes
 // row checkpoints for all four diagonals and no volume at all, and
 // wta_strip_kernel recomputes all eight directions per tile, walking strips
 // of tiles so that every diagonal line runs once (no per-tile halo).
 // kStripTileW: tile columns (16 or 32; 32 x 16 lanes = 512 threads);
 // kStripCols: strip length in columns (rounded to whole tiles, evened out).
+// Built, bit-exact (265 GPU tests with it on) and measured slower
+// (profiles/r06_v2/ab_*.log.txt, frame ms product / strip / 32-wide strip):
+// 1080p D=128 0.883 / 0.962 / 1.078, 1080p D=64 0.542 / 0.705 / 0.782,
+// 640x480 D=64 0.129 / 0.203 / 0.207 -- the final kernel is VALU-issue-bound
+// at 0.83 of the measured mix ceiling.  Off.
 constexpr int kStripRoute = 0;
 constexpr int kStripTileW = 16;
 constexpr int kStripCols = 128;

@@ -471,7 +471,7 @@ hipError_t launch_wta_hv(Ctx& c, const uint8_t* C, const uint8_t* L4, const uint
                          const uint8_t* CKV, int W, int H, int D, int P1, int P2, int dmin,
                          uint16_t* disp, float* sub, int dreal, int npair) {
     // D <= 128 on the strip route: all eight directions recomputed per tile
-    // from checkpoints, no diagonal volume (wta_strip.hip, DESIGN.md §4.12)
+    // from checkpoints, no diagonal volume (wta_strip.hip, DESIGN.md §4.13)
     if (tune::kStripRoute != 0 && wta_strip_supported(D))
         return launch_wta_strip(c, C, CK, CKV, W, H, D, P1, P2, dmin, disp, sub, dreal, npair);
     DispatchTimer t(c, "wta_hv");

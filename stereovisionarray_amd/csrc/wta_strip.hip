@@ -1,6 +1,6 @@
 // wta_strip.hip -- the tile pipeline's final kernel with all eight
-// directions recomputed per tile (DESIGN.md §4.12, SURVEY.md §8a rows
-// A12-A13).  Used at D <= 128.
+// directions recomputed per tile (DESIGN.md §4.13, SURVEY.md §8a rows
+// A12-A13).  Built for D <= 128 when tune::kStripRoute.
 //
 // sgm_paths (checkpoint mode 2 + 3) leaves no path volume at all: only the
 // states of every line at the checkpoint columns / rows (every 8 pixels):
@@ -36,8 +36,12 @@
 //
 // LDS block of pixel (ring column rc, row r): [pair p][lane k] dwords, so 16
 // lanes touch 16 consecutive dwords per pair (conflict-free single-dword
-// atomics).  At D = 128, TW = 32: 40 x 8 x 64 x 4 B = 80 KB, two 512-thread
-// workgroups per CU (4 waves per SIMD).
+// atomics).  At D = 128, TW = 16: 24 x 8 x 64 x 4 B = 48 KB, three workgroups
+// per CU (168 VGPRs, 3 waves per SIMD).
+//
+// MEASURED SLOWER than the wta_hv route and OFF (tune::kStripRoute = 0):
+// 1080p D=128 frame 0.962 vs 0.883 ms, this kernel VALU-issue-bound at 0.83
+// of the measured mix ceiling (profiles/r06_v2/).
 #include "sgm_common.h"
 #include "wta_common.h"
 #include "sva_tuning.h"

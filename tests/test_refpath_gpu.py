@@ -393,3 +393,30 @@ def test_ref_path_limits(ctx, sva):
         assert e.value.status == status
     d8, _, v = ctx.disparity_ref(a, a, cr, co, k=23)        # 2k = 46 < 48: accepted
     assert d8.shape == (H, W)
+
+
+@pytest.mark.parametrize("k", [4, 13, 32])
+@pytest.mark.parametrize("pair", [(12, 11), (12, 6)])
+def test_ref_path_unsplit_other_k(ctx, sva, oracle, plane_split, k, pair):
+    """the unsplit plane loop (direct writes, no keys) at k other
+    than 20, forced through SVA_DEBUG_PLANE_SPLIT = 1."""
+    plane_split(1)
+    test_ref_path_window_sizes(ctx, sva, oracle, k, pair)
+
+
+def test_ref_path_keys_stay_clean_across_calls(ctx, sva, oracle):
+    """ref_finalize_kernel puts every key back to all-ones, so only the first
+    call (or a grown buffer) memsets the key buffer: a u32-key frame, a WIDE
+    (u64-key) frame, a smaller frame and the first again on one context, each
+    bit-exact."""
+    runs = []
+    for (W, H, seed) in ((640, 480, 3), (4160, 64, 4), (320, 240, 5), (640, 480, 3)):
+        cr, co, ocr, oco = cams_for(sva, oracle, W, 12, 11)
+        a = synth.texture(H, W, seed)
+        b = np.roll(a, W // 20, axis=1)
+        d8, d16, valid = ctx.disparity_ref(a, b, cr, co, k=8)
+        o8, o16, ov, _ = oracle.ref_pair(a, b, ocr, oco, k=8)
+        assert ov.sum() > 0
+        assert np.array_equal(valid, ov) and np.array_equal(d16, o16) and np.array_equal(d8, o8)
+        runs.append(d16)
+    assert np.array_equal(runs[0], runs[3])
