@@ -78,6 +78,75 @@ def main():
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
 
+    if "sep" in a.part:
+        # cost volume and diagonal volumes in separate allocations, with a
+        # ballast allocation before them and between them
+        lay = sva.tile_layout(W, H, D)
+        for pre_gb, mid_gb in ((0, 0), (3, 0), (0, 3), (1, 0), (2, 0), (0, 1), (5, 0), (16, 0),
+                               (0, 0)):
+            pre = torch.empty(pre_gb << 30, dtype=torch.uint8, device=dev) if pre_gb else None
+            ctx = sva.Context(0)
+            ctx.set_stream(s.cuda_stream)
+            C = torch.zeros(lay.cost_bytes, dtype=torch.uint8, device=dev)
+            ctx.census_cost_d(dL.data_ptr(), dR.data_ptr(), W, H, W, p, C.data_ptr())
+            mid = torch.empty(mid_gb << 30, dtype=torch.uint8, device=dev) if mid_gb else None
+            dg = torch.empty(lay.diag_bytes, dtype=torch.uint8, device=dev)
+            hk = torch.empty(lay.hckpt_bytes, dtype=torch.uint8, device=dev)
+            vk = torch.empty(lay.vckpt_bytes, dtype=torch.uint8, device=dev)
+            fn = lambda: ctx.paths_tile_d(C.data_ptr(), C.numel(), W, H, p, dg.data_ptr(),
+                                          lay.diag_bytes, hk.data_ptr(), lay.hckpt_bytes,
+                                          vk.data_ptr(), lay.vckpt_bytes)
+            t = timed(ctx, fn, a.iters)
+            G = 1 << 30
+            print(json.dumps({"part": "sep", "pre_gb": pre_gb, "mid_gb": mid_gb,
+                              "C_GB": round(C.data_ptr() / G, 3), "diag_GB": round(dg.data_ptr() / G, 3),
+                              "C_mod_1G_MB": (C.data_ptr() % G) >> 20,
+                              "diag_mod_1G_MB": (dg.data_ptr() % G) >> 20,
+                              "ms": t}), flush=True)
+            ctx.close()
+            del pre, mid, C, dg, hk, vk
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+
+    if "alloc" in a.part:
+        # the same buffers from hipExtMallocWithFlags, default vs physically
+        # contiguous, allocated and freed several times
+        import ctypes as ct
+        hip = None
+        for name in ("libamdhip64.so", "libamdhip64.so.6", "libamdhip64.so.7"):
+            try:
+                hip = ct.CDLL(name)
+                break
+            except OSError:
+                continue
+        hip.hipExtMallocWithFlags.argtypes = [ct.POINTER(ct.c_void_p), ct.c_size_t, ct.c_uint]
+        hip.hipFree.argtypes = [ct.c_void_p]
+        lay = sva.tile_layout(W, H, D)
+        ctx = sva.Context(0)
+        ctx.set_stream(s.cuda_stream)
+        for flags, label in ((0, "default"), (4, "contiguous")) * 3:
+            ptrs = []
+            ok = True
+            for nbytes in (lay.cost_bytes, lay.diag_bytes, lay.hckpt_bytes, lay.vckpt_bytes):
+                pp = ct.c_void_p()
+                st = hip.hipExtMallocWithFlags(ct.byref(pp), nbytes, flags)
+                if st != 0:
+                    ok = False
+                    print(json.dumps({"part": "alloc", "mode": label, "error": st}), flush=True)
+                    break
+                ptrs.append(pp.value)
+            if ok:
+                Cp, dg, hk, vk = ptrs
+                ctx.census_cost_d(dL.data_ptr(), dR.data_ptr(), W, H, W, p, Cp)
+                fn = lambda: ctx.paths_tile_d(Cp, lay.cost_bytes, W, H, p, dg, lay.diag_bytes, hk,
+                                              lay.hckpt_bytes, vk, lay.vckpt_bytes)
+                t = timed(ctx, fn, a.iters)
+                print(json.dumps({"part": "alloc", "mode": label, "ms": t}), flush=True)
+            torch.cuda.synchronize()
+            for pp in ptrs:
+                hip.hipFree(pp)
+        ctx.close()
+
     if "frame" in a.part:
         disp = torch.zeros((H, W), dtype=torch.int16, device=dev)
         sub = torch.zeros((H, W), dtype=torch.float32, device=dev)
