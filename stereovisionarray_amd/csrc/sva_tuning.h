@@ -156,6 +156,12 @@ constexpr int kWtahvSubLds = 1;
 constexpr int kWtahvKeyPerm = 1;
 constexpr int kWtahvSubDeferred = 1;
 // Minimum waves per SIMD asked of the compiler for wta_hv (launch bounds).
+// Round 6: u8 keeps + phase H's cost loads after phase V + a 2-pixel volume
+// prefetch bring D=128 to 90 VGPRs with no scratch, 5 waves/SIMD -- and the
+// kernel does not get faster (1080p D=128 wta_hv 0.2519 ms product vs
+// 0.2578 / 0.2598 / 0.2610 for the three 5-wave variants; D=64 and 640x480
+// within noise; profiles/r06_v7/ab_o5_*): it sits on its instruction-mix
+// ceiling and its bytes at once.
 constexpr int kWtahvMinWaves = 1;
 // LDS V blocks at D = 256 (8 u16 pairs = two 16-byte chunks per lane): 1 swaps
 // a lane's two chunks when ((k >> 2) ^ (k >> 3)) & 1, which makes every
