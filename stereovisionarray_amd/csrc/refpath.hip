@@ -882,7 +882,7 @@ __global__ __launch_bounds__(256, tune::kPlaneMinBlocks) void ref_plane3_kernel(
 // is put back to all-ones, so the next call needs no memset.
 template <class Key>
 __global__ void ref_finalize_kernel(int W, int H, const int4* __restrict__ ends,
-                                    const Key* __restrict__ keys,
+                                    Key* __restrict__ keys,
                                     uint8_t* __restrict__ disp_u8, uint16_t* __restrict__ disp_u16,
                                     uint8_t* __restrict__ valid_out) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
@@ -890,7 +890,7 @@ __global__ void ref_finalize_kernel(int W, int H, const int4* __restrict__ ends,
     const size_t p = (size_t)y * W + x;
     const Key key = keys[p];
     if (key == (Key)~(Key)0) return;
-    const_cast<Key*>(keys)[p] = (Key)~(Key)0;
+    keys[p] = (Key)~(Key)0;
     const int4 e = ends[p];
     int cx, cy;
     line_point(make_line(e.x, e.y, e.z, e.w),
@@ -1027,11 +1027,11 @@ hipError_t launch_ref_match(Ctx& c, const uint8_t* ref, const uint8_t* other, in
     if (split && wide)
         hipLaunchKernelGGL(ref_finalize_kernel<unsigned long long>,
                            dim3((unsigned)((W + 255) / 256), (unsigned)H), dim3(256), 0, c.stream, W,
-                           H, (const int4*)ends, (const unsigned long long*)keys, disp_u8, disp_u16,
+                           H, (const int4*)ends, (unsigned long long*)keys, disp_u8, disp_u16,
                            valid_out);
     else if (split)
         hipLaunchKernelGGL(ref_finalize_kernel<unsigned>, dim3((unsigned)((W + 255) / 256), (unsigned)H),
-                           dim3(256), 0, c.stream, W, H, (const int4*)ends, (const unsigned*)keys,
+                           dim3(256), 0, c.stream, W, H, (const int4*)ends, (unsigned*)keys,
                            disp_u8, disp_u16, valid_out);
     const hipError_t err = hipGetLastError();
     // the finalize pass restores every key of the W x H region to all-ones
