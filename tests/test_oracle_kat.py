@@ -410,3 +410,23 @@ def test_resize_half_kat(oracle):
     assert oracle.resize_half(c).shape == (0, 4)
     d = np.array([[255, 254], [255, 254]], np.uint8)  # (1018+2)>>2 = 255 (no overflow)
     assert oracle.resize_half(d).tolist() == [[255]]
+
+
+def test_mode_r_planes_line_offsets(oracle):
+    """tools/mode_r_planes.py (the bench's sad_planes_per_candidate report)
+    forms each pixel's candidate offsets with the kernel's closed form; they
+    must be the oracle's Bresenham points relative to the pixel, in order."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "mode_r_planes", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                      "tools", "mode_r_planes.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    rng = np.random.RandomState(5)
+    for _ in range(2000):
+        x, y = (int(v) for v in rng.randint(0, 100, 2))
+        a = tuple(int(v) for v in rng.randint(-60, 160, 2))
+        b = tuple(int(v) for v in rng.randint(-60, 160, 2))
+        want = [(px - x, py - y) for px, py in oracle.bresenham(a, b)]
+        assert m.line_offsets(x, y, a, b) == want, (x, y, a, b)
