@@ -173,6 +173,68 @@ __device__ __forceinline__ unsigned lane_min_u16(const unsigned (&A)[NP]) {
     return mf.x < mf.y ? mf.x : mf.y;
 }
 
+// ---- pair layout of the recurrence state (tune::kSplitPairs, §4.14) -------
+// Lane k holds its DPL disparities as NP = DPL/2 packed u16 pairs.  Local
+// disparity e (0 <= e < DPL) sits in pair pair_of(e), half half_of(e);
+// pair_d(j, h) is the inverse.  Split: pair j = (e = j, e = j + NP).
+// Adjacent: pair j = (2j, 2j + 1).
+template <int DPL> __host__ __device__ constexpr int pair_d(int j, int h) {
+    return tune::kSplitPairs ? j + h * (DPL / 2) : 2 * j + h;
+}
+template <int DPL> __host__ __device__ constexpr int pair_of(int e) {
+    return tune::kSplitPairs ? e % (DPL / 2) : e >> 1;
+}
+template <int DPL> __host__ __device__ constexpr int half_of(int e) {
+    return tune::kSplitPairs ? e / (DPL / 2) : e & 1;
+}
+
+// d-ordered u8 words (C, L_r volumes, checkpoints) -> state-layout pairs:
+// one v_perm per pair in both layouts.
+template <int DPL>
+__device__ __forceinline__ void words_to_pairs(const unsigned (&w)[DPL / 4], unsigned (&A)[DPL / 2]) {
+    constexpr int NW = DPL / 4, NP = DPL / 2;
+    if constexpr (tune::kSplitPairs != 0) {
+#pragma unroll
+        for (int j = 0; j < NP; j++) {
+            constexpr unsigned Z = 0x0cu;     // v_perm selector: zero byte
+            const int el = j, eh = j + NP;
+            const unsigned sel = (unsigned)(el & 3) | (Z << 8) | ((4u + (unsigned)(eh & 3)) << 16) | (Z << 24);
+            A[j] = __builtin_amdgcn_perm(w[eh >> 2], w[el >> 2], sel);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < NW; q++) unpack4(w[q], A[2 * q], A[2 * q + 1]);
+    }
+}
+
+// State-layout pairs (values < 256) -> d-ordered u8 words.  Split: pairs
+// (2i, 2i + 1) first merge into T_i = (A_2i.lo, A_2i+1.lo, A_2i.hi,
+// A_2i+1.hi) bytes, then each word takes two byte pairs of two T's.
+template <int DPL>
+__device__ __forceinline__ void pairs_to_words(const unsigned (&A)[DPL / 2], unsigned (&ow)[DPL / 4]) {
+    constexpr int NW = DPL / 4, NP = DPL / 2;
+    if constexpr (tune::kSplitPairs != 0) {
+        unsigned T[NP / 2];
+#pragma unroll
+        for (int i = 0; i < NP / 2; i++) T[i] = __builtin_amdgcn_perm(A[2 * i + 1], A[2 * i], 0x06020400u);
+        if constexpr (NP == 2) {
+            ow[0] = T[0];                     // (d0, d2), (d1, d3) -> d0 d1 d2 d3
+        } else {
+#pragma unroll
+            for (int q = 0; q < NW; q++) {
+                const int e0 = 4 * q, e2 = 4 * q + 2;
+                const int a = (e0 % NP) / 2, ha = e0 / NP, b = (e2 % NP) / 2, hb = e2 / NP;
+                const unsigned sel = (unsigned)(2 * ha) | ((unsigned)(2 * ha + 1) << 8) |
+                                     ((unsigned)(4 + 2 * hb) << 16) | ((unsigned)(5 + 2 * hb) << 24);
+                ow[q] = __builtin_amdgcn_perm(T[b], T[a], sel);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int w = 0; w < NW; w++) ow[w] = pack4(A[2 * w], A[2 * w + 1]);
+    }
+}
+
 // One recurrence step for the lane's DPL disparities.  State A = L(q, .)
 // (unnormalised u16 pairs), m = min_k L(q, k) broadcast over the row.
 //   u      = min(min(A(d-1), A(d+1)) + P1, A(d), m + P2)      (all >= m)
@@ -192,16 +254,36 @@ template <int DPL, bool PIN = false>
 __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigned (&A)[DPL / 2],
                                            unsigned& m, unsigned (&ow)[DPL / 4], unsigned P1,
                                            unsigned P2, Edges& e) {
-    constexpr int NW = DPL / 4, NP = DPL / 2;
-    // neighbours: X = lane k-1's last pair, Y = lane k+1's first pair
+    constexpr int NP = DPL / 2;
+    // neighbours: X = lane k-1's last pair, Y = lane k+1's first pair (its
+    // high half holds L(d0 - 1) and its low half L(d0 + DPL) in both layouts)
     e.X = row_shr1(A[NP - 1], e.X);
     e.Y = row_shl1(A[0], e.Y);
     const unsigned X = e.X, Y = e.Y;
-    unsigned M[NP];
-    M[0] = __builtin_amdgcn_alignbit(A[0], X, 16);
+    // lo[j] / hi[j]: the pairs whose min is pair j's min(A(d-1), A(d+1))
+    unsigned lo[NP], hi[NP];
+    if constexpr (tune::kSplitPairs != 0) {
+        // pair j = (j, j + NP): its d-1 pair is pair j-1 and its d+1 pair is
+        // pair j+1, whole registers, except (X.hi, A[NP-1].lo) for j = 0 and
+        // (A[0].hi, Y.lo) for j = NP-1
 #pragma unroll
-    for (int j = 1; j < NP; j++) M[j] = __builtin_amdgcn_alignbit(A[j], A[j - 1], 16);
-    const unsigned Qlast = __builtin_amdgcn_alignbit(Y, A[NP - 1], 16);
+        for (int j = 0; j < NP; j++) {
+            lo[j] = j == 0 ? __builtin_amdgcn_alignbit(A[NP - 1], X, 16) : A[j - 1];
+            hi[j] = j == NP - 1 ? __builtin_amdgcn_alignbit(Y, A[0], 16) : A[j + 1];
+        }
+    } else {
+        // pair j = (2j, 2j+1): d-1 is (A[j-1].hi, A[j].lo), d+1 the next one
+        unsigned M[NP];
+        M[0] = __builtin_amdgcn_alignbit(A[0], X, 16);
+#pragma unroll
+        for (int j = 1; j < NP; j++) M[j] = __builtin_amdgcn_alignbit(A[j], A[j - 1], 16);
+        const unsigned Qlast = __builtin_amdgcn_alignbit(Y, A[NP - 1], 16);
+#pragma unroll
+        for (int j = 0; j < NP; j++) {
+            lo[j] = M[j];
+            hi[j] = j < NP - 1 ? M[j + 1] : Qlast;
+        }
+    }
     // K = -(m * 0x10001) in one v_mul_i32_i24 (m < 2^10; the literal's low 24
     // bits are -65537), and m + P2 in both halves = P2 * 0x10001 - K: two VALU
     // where m | m << 16, its negation and the sum took three plus a copy of P2
@@ -213,7 +295,7 @@ __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigne
     // instruction (gfx950 puts an s_nop between dependent VOP3P ops).
     u16x2 t[NP];
 #pragma unroll
-    for (int j = 0; j < NP; j++) t[j] = vmin2(as_v2(M[j]), as_v2(j < NP - 1 ? M[j + 1] : Qlast));
+    for (int j = 0; j < NP; j++) t[j] = vmin2(as_v2(lo[j]), as_v2(hi[j]));
     unsigned tp[NP];
     if constexpr (tune::kStepAddU32 != 0) {
         // + P1 in both halves as ONE 32-bit add (VOP2, full issue rate; the
@@ -229,8 +311,7 @@ __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigne
     }
 #pragma unroll
     for (int j = 0; j < NP; j++) A[j] = add3(min3_u16x2(tp[j], A[j], mP2), c[j], K);
-#pragma unroll
-    for (int w = 0; w < NW; w++) ow[w] = pack4(A[2 * w], A[2 * w + 1]);
+    pairs_to_words<DPL>(A, ow);
     m = row_min_u32<PIN>(lane_min_u16<NP>(A));
 }
 
@@ -248,8 +329,7 @@ __device__ __forceinline__ void sgm_step(const unsigned (&cw)[DPL / 4], unsigned
                                          unsigned& m, unsigned (&ow)[DPL / 4], unsigned P1,
                                          unsigned P2, Edges& e) {
     unsigned c[DPL / 2];
-#pragma unroll
-    for (int w = 0; w < DPL / 4; w++) unpack4(cw[w], c[2 * w], c[2 * w + 1]);
+    words_to_pairs<DPL>(cw, c);
     sgm_step_c<DPL, PIN>(c, A, m, ow, P1, P2, e);
 }
 
@@ -482,15 +562,13 @@ __device__ __forceinline__ void path_line(rsrc_t rC, rsrc_t rL, const PathGeom& 
 
 // ---- shared by the final kernels (wta.hip, wta_hv.hip) ---------------------
 
+// S += the d-ordered u8 words w, in the state's pair layout.
 template <int NW>
 __device__ __forceinline__ void unpack_add(const unsigned (&w)[NW], unsigned (&S)[2 * NW]) {
+    unsigned a[2 * NW];
+    words_to_pairs<4 * NW>(w, a);
 #pragma unroll
-    for (int q = 0; q < NW; q++) {
-        unsigned a, b;
-        unpack4(w[q], a, b);
-        S[2 * q] += a;        // packed add: S <= 8 * 255 < 2^16 per half, no carry
-        S[2 * q + 1] += b;
-    }
+    for (int j = 0; j < 2 * NW; j++) S[j] += a[j];   // packed add: S <= 8 * 255 < 2^16 per half, no carry
 }
 
 // Path state from a u8 checkpoint: A = L(q) as packed pairs, m = min_k L(q).
@@ -501,9 +579,8 @@ __device__ __forceinline__ void unpack_add(const unsigned (&w)[NW], unsigned (&S
 template <int DPL, bool PAD, bool PIN = false>
 __device__ __forceinline__ void state_from_words(const Words<DPL / 4>& w, unsigned (&A)[DPL / 2],
                                                  unsigned& m, const unsigned (&padm)[DPL / 2]) {
-    constexpr int NW = DPL / 4, NP = DPL / 2;
-#pragma unroll
-    for (int q = 0; q < NW; q++) unpack4(w.w[q], A[2 * q], A[2 * q + 1]);
+    constexpr int NP = DPL / 2;
+    words_to_pairs<DPL>(w.w, A);
     if constexpr (PAD) {
 #pragma unroll
         for (int j = 0; j < NP; j++) A[j] |= padm[j] & 0x00ff00ffu;   // A < 256: OR = max

@@ -17,6 +17,18 @@ namespace tune {
 // v_pk_add_u16 (0): VOP2 issues at ~2x the rate of VOP3P on gfx950
 // (profiles/r06_v1/microbench_valu.txt).
 constexpr int kStepAddU32 = 1;
+// Pair layout of the recurrence state: pair j of lane k
+// holds disparities (k*DPL + j, k*DPL + j + DPL/2) (1, "split") instead of
+// (k*DPL + 2j, k*DPL + 2j + 1) (0).  Split pairs have their d-1 / d+1
+// neighbours in whole registers, so the step needs 2 v_alignbit instead of
+// DPL/2 + 1; packing a u8 volume word costs 2 v_perm instead of 1.  HBM
+// formats (C, L_r volumes, checkpoints) stay in d order either way.  Static
+// VALU of wta_hv D=64/128/192/256 -3.3/-5.9/-6.8/-7.6 %; in-process A/B,
+// frame ms split / adjacent (profiles/r06_v8/, two runs): 1080p D=128 0.8817
+// / 0.8828 and 0.8772 / 0.8792, D=64 0.5082 / 0.5175 and 0.5053 / 0.5116
+// (sgm_paths -2.5 %), D=192 1.3132 / 1.3205, D=256 1.7015 / 1.7098 and
+// 1.6991 / 1.7094, 640x480 D=64 0.1260 / 0.1276 and 0.1274 / 0.1297.
+constexpr int kSplitPairs = 1;
 // Prefetch ring depth in steps, per line kind and disparities per lane
 // (D = 16 * DPL).  Horizontal lines are few (2H) and long (W steps) and run
 // alone once the vertical/diagonal lines drain, so they get the deeper ring.
@@ -155,6 +167,15 @@ constexpr int kWtahvSubLds = 1;
 // exec-masked read block per pixel.
 constexpr int kWtahvKeyPerm = 1;
 constexpr int kWtahvSubDeferred = 1;
+// Round 6: each pixel's cost words expanded to u16 pairs once per phase and
+// kept for the phase's second recurrence (down/up, left/right) instead of
+// twice; bit b for DPL = 4 (b + 1).  Costs NP VGPRs per row of the tile
+// (D=128: 111 -> 129, 4 -> 3 waves/SIMD, so never there).  Measured with
+// bits 0 and 3 (D=64, D=256), wta_hv ms on / off (profiles/r06_v8/r7l_ab_*):
+// 1080p D=64 0.1423 / 0.1421, D=256 0.4830 / 0.4862, 640x480 D=64 0.0261 /
+// 0.0268, 4K D=256 1.9735 / 1.9745 -- noise: the kernel streams its bytes at
+// ~5.9 TB/s, and fewer VALU do not move it.  Off.
+constexpr int kWtahvUnpackOnce = 0;
 // Minimum waves per SIMD asked of the compiler for wta_hv (launch bounds).
 // Round 6: u8 keeps + phase H's cost loads after phase V + a 2-pixel volume
 // prefetch bring D=128 to 90 VGPRs with no scratch, 5 waves/SIMD -- and the

@@ -65,6 +65,8 @@ __global__ __launch_bounds__(TB, tune::kWtahvMinWaves) void wta_hv_kernel(const 
     constexpr int KEEPM = DPL <= 8 ? tune::kWtahvKeepU16 : tune::kWtahvKeepU16Wide;
     constexpr bool KEEP16 = (KEEPM & 1) != 0, KEEP16H = (KEEPM & 2) != 0;
     constexpr bool PIN = tune::kWtahvPinRowMin != 0;     // row_min_u32<PIN>
+    // cost words expanded once per phase (tune::kWtahvUnpackOnce)
+    constexpr bool UNPACK1 = ((tune::kWtahvUnpackOnce >> (DPL / 4 - 1)) & 1) != 0;
 
     constexpr int SPR = TW / TY;        // phase H: row segments per tile row
     static_assert(TY <= TW && TW % TY == 0, "tile rows must divide 16");
@@ -96,8 +98,8 @@ __global__ __launch_bounds__(TB, tune::kWtahvMinWaves) void wta_hv_kernel(const 
     unsigned padm[NP];
 #pragma unroll
     for (int j = 0; j < NP; j++) {
-        const int d = k * DPL + 2 * j;
-        padm[j] = PAD ? ((d >= g.dreal ? 0x0000ffffu : 0u) | (d + 1 >= g.dreal ? 0xffff0000u : 0u))
+        const int dl = k * DPL + pair_d<DPL>(j, 0), dh = k * DPL + pair_d<DPL>(j, 1);
+        padm[j] = PAD ? ((dl >= g.dreal ? 0x0000ffffu : 0u) | (dh >= g.dreal ? 0xffff0000u : 0u))
                       : 0u;
     }
 
@@ -171,8 +173,7 @@ __global__ __launch_bounds__(TB, tune::kWtahvMinWaves) void wta_hv_kernel(const 
 #pragma unroll
                 for (int p = 0; p < NP; p++) V[p] = ld[p] + Au[p];   // L_2 + L_3 (<= 510 per half)
             } else {
-#pragma unroll
-                for (int q = 0; q < NW; q++) unpack4(ld[q], V[2 * q], V[2 * q + 1]);
+                words_to_pairs<DPL>(ld, V);
                 unpack_add<NW>(lu, V);
             }
             unsigned* dst = &vsum[(r * TW + slot) * 16 * NP];
@@ -201,16 +202,26 @@ __global__ __launch_bounds__(TB, tune::kWtahvMinWaves) void wta_hv_kernel(const 
                 }
             });
         } else {
+            unsigned cvp[UNPACK1 ? TY : 1][NP];           // row r's cost pairs (UNPACK1)
             for_seq<TY>([&](auto I) {
                 constexpr int i = decltype(I)::value;
                 unsigned ow[NW];
-                if (i < ny) { sgm_step<DPL, PIN>(cv[i].w, Aa, ma, ow, P1, P2, ea); keep(LD[i], Aa, ow); }
+                if (i < ny) {
+                    if constexpr (UNPACK1) {
+                        words_to_pairs<DPL>(cv[i].w, cvp[i]);
+                        sgm_step_c<DPL, PIN>(cvp[i], Aa, ma, ow, P1, P2, ea);
+                    } else {
+                        sgm_step<DPL, PIN>(cv[i].w, Aa, ma, ow, P1, P2, ea);
+                    }
+                    keep(LD[i], Aa, ow);
+                }
             });
             for_seq<TY>([&](auto Q) {
                 constexpr int r = TY - 1 - decltype(Q)::value;
                 if (r < ny) {
                     unsigned lu[NW];
-                    sgm_step<DPL, PIN>(cv[r].w, Ab, mb, lu, P1, P2, eb);
+                    if constexpr (UNPACK1) sgm_step_c<DPL, PIN>(cvp[UNPACK1 ? r : 0], Ab, mb, lu, P1, P2, eb);
+                    else sgm_step<DPL, PIN>(cv[r].w, Ab, mb, lu, P1, P2, eb);
                     put_v(r, LD[r], Ab, lu);
                 }
             });
@@ -344,11 +355,17 @@ __global__ __launch_bounds__(TB, tune::kWtahvMinWaves) void wta_hv_kernel(const 
     // L_0 of the segment's pixels, kept like phase V's L_2 (KEEP16H)
     constexpr int NKH = KEEP16H ? NP : NW;
     unsigned LF[TY][NKH];
+    unsigned chp[UNPACK1 ? TY : 1][NP];                // pixel i's cost pairs (UNPACK1)
     for_seq<TY>([&](auto I) {
         constexpr int i = decltype(I)::value;
         unsigned ow[NW];
         if (i < nh) {
-            sgm_step<DPL, PIN>(ch[i].w, Aa, ma, ow, P1, P2, ea);
+            if constexpr (UNPACK1) {
+                words_to_pairs<DPL>(ch[i].w, chp[i]);
+                sgm_step_c<DPL, PIN>(chp[i], Aa, ma, ow, P1, P2, ea);
+            } else {
+                sgm_step<DPL, PIN>(ch[i].w, Aa, ma, ow, P1, P2, ea);
+            }
 #pragma unroll
             for (int q = 0; q < NKH; q++) LF[i][q] = KEEP16H ? Aa[q] : ow[q];
         }
@@ -357,16 +374,18 @@ __global__ __launch_bounds__(TB, tune::kWtahvMinWaves) void wta_hv_kernel(const 
     else zero_state(Aa, ma);
     unsigned dres = 0u, sm = 0u, s0 = 0u;
     const bool want_sub = sub != nullptr;
-    unsigned dpair[NP];                                // (d, d + 1) of each pair (kWtahvKeyPerm)
+    unsigned dpair[NP];                                // each pair's two d (kWtahvKeyPerm)
 #pragma unroll
-    for (int j = 0; j < NP; j++) dpair[j] = (lane_d + 2u * j) | ((lane_d + 2u * j + 1u) << 16);
+    for (int j = 0; j < NP; j++)
+        dpair[j] = (lane_d + (unsigned)pair_d<DPL>(j, 0)) | ((lane_d + (unsigned)pair_d<DPL>(j, 1)) << 16);
     constexpr bool DEFER = tune::kWtahvSubLds != 0 && tune::kWtahvSubDeferred != 0;
     unsigned* const vrow = &vsum[(hr * TW + hseg * TY) * 16 * NP];   // the segment's V blocks
     for_seq<TY>([&](auto Q) {
         constexpr int q = decltype(Q)::value, j = TY - 1 - q, s = q % kPfVol;
         if (j < nh) {
             unsigned ow[NW];
-            sgm_step<DPL, PIN>(ch[j].w, Aa, ma, ow, P1, P2, ea);
+            if constexpr (UNPACK1) sgm_step_c<DPL, PIN>(chp[UNPACK1 ? j : 0], Aa, ma, ow, P1, P2, ea);
+            else sgm_step<DPL, PIN>(ch[j].w, Aa, ma, ow, P1, P2, ea);
             unsigned* const vpix = vrow + j * 16 * NP;                     // this pixel's V
             unsigned S[NP];
 #pragma unroll
@@ -391,7 +410,7 @@ __global__ __launch_bounds__(TB, tune::kWtahvMinWaves) void wta_hv_kernel(const 
                 // the two neighbours (same wave, behind a wave barrier).
                 const unsigned best = tune::kWtahvKeyPerm
                                           ? wta_pick_key_perm<DPL, PIN && tune::kWtahvPinWta>(S, dpair)
-                                          : wta_pick_key<DPL, PIN && tune::kWtahvPinWta>(S, k);
+                                          : wta_pick_key<DPL, PIN && tune::kWtahvPinWta, tune::kSplitPairs != 0>(S, k);
                 const int ds = (int)(best & 0xffffu);
                 if (want_sub) {
 #pragma unroll
@@ -416,14 +435,14 @@ __global__ __launch_bounds__(TB, tune::kWtahvMinWaves) void wta_hv_kernel(const 
                         const int dm = ds > 0 ? ds - 1 : 0, dp = ds + 1 < 16 * DPL ? ds + 1 : ds;
                         // u16 of disparity d: pair (d / 2) % NP of lane d / DPL
                         auto at = [&](int d) {
-                            const int kk = d / DPL, pp = (d >> 1) % NP;
-                            return (unsigned)s16[2 * (kk * NP + (pp ^ vsw_of(kk))) + (d & 1)];
+                            const int kk = d / DPL, pp = pair_of<DPL>(d % DPL), hh = half_of<DPL>(d % DPL);
+                            return (unsigned)s16[2 * (kk * NP + (pp ^ vsw_of(kk))) + hh];
                         };
                         sm = at(dm) | (at(dp) << 16);
                     }
                 }
             } else {
-                const int ds = wta_pick_raw<DPL, PIN && tune::kWtahvPinWta>(S, k, want_sub, &spm, &sb);
+                const int ds = wta_pick_raw<DPL, PIN && tune::kWtahvPinWta, tune::kSplitPairs != 0>(S, k, want_sub, &spm, &sb);
                 if (k == j) {
                     dres = (unsigned)ds;
                     sm = spm;
@@ -449,8 +468,8 @@ __global__ __launch_bounds__(TB, tune::kWtahvMinWaves) void wta_hv_kernel(const 
                 const int ds = (int)dres;
                 const int dm = ds > 0 ? ds - 1 : 0, dp = ds + 1 < 16 * DPL ? ds + 1 : ds;
                 auto at = [&](int d) {
-                    const int kk = d / DPL, pp = (d >> 1) % NP;
-                    return (unsigned)s16[2 * (kk * NP + (pp ^ vsw_of(kk))) + (d & 1)];
+                    const int kk = d / DPL, pp = pair_of<DPL>(d % DPL), hh = half_of<DPL>(d % DPL);
+                    return (unsigned)s16[2 * (kk * NP + (pp ^ vsw_of(kk))) + hh];
                 };
                 sm = at(dm) | (at(dp) << 16);
             }

@@ -105,8 +105,8 @@ __global__ __launch_bounds__(TW * 16, tune::kStripMinWaves) void wta_strip_kerne
     unsigned padm[NP];
 #pragma unroll
     for (int j = 0; j < NP; j++) {
-        const int d = k * DPL + 2 * j;
-        padm[j] = PAD ? ((d >= g.dreal ? 0x0000ffffu : 0u) | (d + 1 >= g.dreal ? 0xffff0000u : 0u))
+        const int dl = k * DPL + pair_d<DPL>(j, 0), dh = k * DPL + pair_d<DPL>(j, 1);
+        padm[j] = PAD ? ((dl >= g.dreal ? 0x0000ffffu : 0u) | (dh >= g.dreal ? 0xffff0000u : 0u))
                       : 0u;
     }
     // has an up checkpoint row (the band is not the image's last)
@@ -224,9 +224,10 @@ __global__ __launch_bounds__(TW * 16, tune::kStripMinWaves) void wta_strip_kerne
 
     const int hr = slot / SPR, hseg = slot % SPR;     // phase H: row hr, segment hseg
     const unsigned yh = (unsigned)(y0 + hr);
-    unsigned dpair[NP];                               // (d, d + 1) of each pair (kWtahvKeyPerm)
+    unsigned dpair[NP];                               // each pair's two d (kWtahvKeyPerm)
 #pragma unroll
-    for (int j = 0; j < NP; j++) dpair[j] = (lane_d + 2u * j) | ((lane_d + 2u * j + 1u) << 16);
+    for (int j = 0; j < NP; j++)
+        dpair[j] = (lane_d + (unsigned)pair_d<DPL>(j, 0)) | ((lane_d + (unsigned)pair_d<DPL>(j, 1)) << 16);
     const bool want_sub = sub != nullptr;
     const rsrc_t rCK0 = make_rsrc(CK, g.hck), rCK1 = make_rsrc(CK + g.hck, g.hck);
 
@@ -376,8 +377,8 @@ __global__ __launch_bounds__(TW * 16, tune::kStripMinWaves) void wta_strip_kerne
                     const int dm = ds > 0 ? ds - 1 : 0, dp = ds + 1 < 16 * DPL ? ds + 1 : ds;
                     // u16 of disparity d: pair (d / 2) % NP of lane d / DPL
                     auto at = [&](int d) {
-                        const int kk = d / DPL, pp = (d >> 1) % NP;
-                        return (unsigned)s16[2 * (pp * 16 + kk) + (d & 1)];
+                        const int kk = d / DPL, pp = pair_of<DPL>(d % DPL), hh = half_of<DPL>(d % DPL);
+                        return (unsigned)s16[2 * (pp * 16 + kk) + hh];
                     };
                     sm = at(dm) | (at(dp) << 16);
                 }
