@@ -102,6 +102,10 @@ def parse():
     ap.add_argument("--rehearse-rccl", action="store_true",
                     help="N=1 only: a 1-rank RCCL process group runs the real overlapped "
                          "gather_maps on the comm stream (the N>1 code path on one GPU)")
+    ap.add_argument("--placement-trials", type=int, default=0,
+                    help="stage-buffer sets sva_reserve's placement check times (0: the "
+                         "library default, which checks only frames with >= 4 GiB of stage "
+                         "buffers; 1: no check)")
     ap.add_argument("--engine", default="auto", choices=["auto", "multi"],
                     help="auto: --gpus N > 1 without torch.distributed.run drives the N devices "
                          "from this one process through the C-ABI engine (sva_multi_create + "
@@ -341,6 +345,24 @@ def mode_r_roofline(mr):
     out["model"] = ("SQ_INSTS_VALU / (ref_match time x 1,024 SIMDs x 2.4 GHz / 2 cycles per "
                     "wave64 VALU instruction)")
     return out
+
+
+def placement_report(ctxs):
+    """sva_reserve's placement check (include/sva.h): per context, the path
+    kernel's time on the stage-buffer set it kept and on the slowest set it
+    timed; None when no context ran the check (stage buffers below 4 GiB)."""
+    import stereovisionarray_amd as sva
+    rows = []
+    for c in ctxs:
+        kept = c.get_debug(sva.SVA_DEBUG_PLACEMENT_NS)
+        if kept > 0:
+            rows.append({"kept_ms": round(kept * 1e-6, 4),
+                         "worst_ms": round(c.get_debug(sva.SVA_DEBUG_PLACEMENT_WORST_NS) * 1e-6, 4)})
+    if not rows:
+        return None
+    return {"contexts": rows,
+            "note": "sgm_paths on each trial allocation of the cost / path / checkpoint buffers at "
+                    "sva_reserve, best of 3 launches; the fastest set is kept (DESIGN.md §6.0000)"}
 
 
 def frame_overlap_beside(W, H, D, frames=40, rounds=2):
@@ -1344,6 +1366,7 @@ def main():
     stream = torch.cuda.Stream(dev)     # non-default stream shared by kernels, copies, RCCL
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
+    ctx.set_debug(sva.SVA_DEBUG_PLACEMENT_TRIALS, a.placement_trials)
     ctx.reserve(W, H, D)
     # --streams S: pair j of a step runs on context j % S (own stream and
     # workspaces); the step's maps are complete once `stream` has waited on all
@@ -1352,6 +1375,7 @@ def main():
         s_ = torch.cuda.Stream(dev)
         c_ = sva.Context(local)
         c_.set_stream(s_.cuda_stream)
+        c_.set_debug(sva.SVA_DEBUG_PLACEMENT_TRIALS, a.placement_trials)
         c_.reserve(W, H, D)
         ctxs.append(c_)
         cstreams.append(s_)
@@ -1481,6 +1505,9 @@ def main():
     }
     if len(ctxs) == 1:
         out["frame_roofline"] = frame_roofline(W, H, D, ms_per_step / P)
+    pl = placement_report(ctxs)
+    if pl:
+        out["placement"] = pl
     if exchange is not None:
         out["exchange"] = exchange
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

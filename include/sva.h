@@ -97,7 +97,14 @@ int sva_set_stream(void* ctx, void* hip_stream);
 int sva_synchronize(void* ctx);
 const char* sva_last_error(void* ctx);
 const char* sva_status_string(int status);
-/* Pre-size the workspace for W x H x D (optional; calls grow it on demand). */
+/* Pre-size the workspace for W x H x D (optional; calls grow it on demand).
+ * When the frame's stage buffers (cost volume, diagonal path volumes,
+ * checkpoints) reach 4 GiB, reserve also checks their placement: it times the
+ * path kernel on the buffers it got and on up to three further allocations of
+ * them, keeps the fastest set and frees the others (at 4K
+ * D=256 the kernel's rate depends on which physical pages the 10.6 GB of
+ * volumes land on, 4.3-4.9 ms, and not on anything else measured).  A few
+ * tens of ms, once; SVA_DEBUG_PLACEMENT_TRIALS sets the count (1 = off). */
 int sva_reserve(void* ctx, int width, int height, int D);
 
 /* Path-aggregation route of sva_disparity_sgm*.  COST_VOLUME (= AUTO, the
@@ -142,10 +149,18 @@ int sva_kernel_time(void* ctx, const char* name, double* total_ms, int64_t* coun
  *                            side-stream join test).
  *   SVA_DEBUG_SIDE_IDLE      get: 1 if every side stream of the batch route
  *                            has finished its queued work (hipStreamQuery),
- *                            else 0. */
+ *                            else 0.
+ *   SVA_DEBUG_PLACEMENT_TRIALS  set: buffer sets sva_reserve's placement check
+ *                            times (1..8; 1 = no check; 0 = the default, 4).
+ *   SVA_DEBUG_PLACEMENT_NS   get: the path kernel's time on the set the last
+ *                            check kept, ns (0: no check ran).
+ *   SVA_DEBUG_PLACEMENT_WORST_NS  get: the slowest set that check timed, ns. */
 #define SVA_DEBUG_PLANE_SPLIT 1
 #define SVA_DEBUG_FAIL_COST_AT 2
 #define SVA_DEBUG_SIDE_IDLE 3
+#define SVA_DEBUG_PLACEMENT_TRIALS 4
+#define SVA_DEBUG_PLACEMENT_NS 5
+#define SVA_DEBUG_PLACEMENT_WORST_NS 6
 int sva_set_debug(void* ctx, int key, int64_t value);
 int sva_get_debug(void* ctx, int key, int64_t* value);
 

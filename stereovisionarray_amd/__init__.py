@@ -37,6 +37,9 @@ SVA_TIMING_AGG = 3
 SVA_DEBUG_PLANE_SPLIT = 1
 SVA_DEBUG_FAIL_COST_AT = 2
 SVA_DEBUG_SIDE_IDLE = 3
+SVA_DEBUG_PLACEMENT_TRIALS = 4
+SVA_DEBUG_PLACEMENT_NS = 5
+SVA_DEBUG_PLACEMENT_WORST_NS = 6
 # The ABI this binding is written against (include/sva.h SVA_ABI_VERSION).
 ABI_VERSION = 6
 
@@ -338,7 +341,8 @@ class Context:
         self._chk(lib.sva_reset_timing(self.h))
 
     def set_debug(self, key: int, value: int):
-        """sva_set_debug: SVA_DEBUG_PLANE_SPLIT / SVA_DEBUG_FAIL_COST_AT (tests)."""
+        """sva_set_debug: SVA_DEBUG_PLANE_SPLIT / SVA_DEBUG_FAIL_COST_AT (tests),
+        SVA_DEBUG_PLACEMENT_TRIALS (sva_reserve's placement check)."""
         self._chk(lib.sva_set_debug(self.h, key, int(value)))
 
     def get_debug(self, key: int) -> int:

@@ -86,6 +86,10 @@ struct Ctx {
     // failure (1-based frame of the next call, 0 = off)
     int dbg_plane_split = 0;
     int dbg_fail_cost_at = 0;
+    // sva_reserve's placement check: sets to time (0 = tune::kPlacementTrials),
+    // and the kept / slowest set's path-kernel time of the last check (ns)
+    int placement_trials = 0;
+    int64_t placement_ns = 0, placement_worst_ns = 0;
 };
 
 // Which launches a timing mode records: SVA_TIMING_ALL every one,

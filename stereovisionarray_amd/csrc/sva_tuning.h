@@ -211,6 +211,15 @@ constexpr int kBatchCostStreams = 3;
 constexpr int kBatchSubFrames = 4;
 constexpr size_t kBatchMaxBytes = (size_t)24 << 30;
 
+// ---- sva_reserve's placement check ----------------------
+// Buffer sets timed (the first allocation plus trials - 1 more) when a frame's
+// stage buffers reach kPlacementMinBytes.  At 4K D=256 the path kernel ran
+// 4.28-4.98 ms on twelve allocations of the same buffers, stable within each
+// (profiles/r06_v6/probe_4k_alloc.log.txt); 1080p D=128 (1.6 GB) shows no
+// such spread.
+constexpr int kPlacementTrials = 4;
+constexpr size_t kPlacementMinBytes = (size_t)4 << 30;
+
 // ---- census.hip / census_cost.hip / cost.hip ------------
 // Rows per workgroup of the multi-row census kernel.
 constexpr int kCensusRows = 16;

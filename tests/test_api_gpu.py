@@ -164,3 +164,55 @@ def test_reserve_timing_and_errors(ctx, sva):
         ctx.disparity_sgm(L, R, sva.default_params(D=300))
     assert "D in 1..256" in str(e.value)
     assert b"D in" in sva.lib.sva_last_error(ctx.h)
+
+
+def test_reserve_placement_check(sva, torch_dev):
+    """sva_reserve's placement check (>= 4 GiB of stage buffers, include/sva.h):
+    it times the path kernel on several allocations of the cost / path /
+    checkpoint buffers and keeps the fastest.  The frame computed afterwards
+    equals one from a context that skipped the check; the trials' launches
+    never reach the kernel timer; small reservations and trials = 1 skip it."""
+    W, H, D = 3840, 2160, 256
+    a, b, c = sva.Context(0), sva.Context(0), sva.Context(0)
+    try:
+        streams = []
+        for x in (a, b, c):
+            s = torch.cuda.current_stream(torch_dev)
+            x.set_stream(s.cuda_stream)
+            streams.append(s)
+        a.set_debug(sva.SVA_DEBUG_PLACEMENT_TRIALS, 3)
+        assert a.get_debug(sva.SVA_DEBUG_PLACEMENT_TRIALS) == 3
+        a.set_timing(True)
+        a.reset_timing()
+        a.reserve(W, H, D)
+        assert a.kernel_time("sgm_paths") == (0.0, 0)
+        a.set_timing(False)
+        kept = a.get_debug(sva.SVA_DEBUG_PLACEMENT_NS)
+        worst = a.get_debug(sva.SVA_DEBUG_PLACEMENT_WORST_NS)
+        assert 0 < kept <= worst
+        assert 1e5 < kept < 1e8                      # 0.1-100 ms: a real 4K D=256 launch
+        b.set_debug(sva.SVA_DEBUG_PLACEMENT_TRIALS, 1)
+        b.reserve(W, H, D)
+        assert b.get_debug(sva.SVA_DEBUG_PLACEMENT_NS) == 0
+        c.reserve(640, 480, 64)                      # 0.1 GB of stage buffers: no check
+        assert c.get_debug(sva.SVA_DEBUG_PLACEMENT_NS) == 0
+        with pytest.raises(sva.SvaError):
+            c.set_debug(sva.SVA_DEBUG_PLACEMENT_TRIALS, 9)
+        with pytest.raises(sva.SvaError):
+            c.set_debug(sva.SVA_DEBUG_PLACEMENT_NS, 1)   # read-only
+        L, R, _ = synth.stereo_pair(H, W, D, 0, -1, seed=5)
+        dL, dR = dev(L, torch_dev), dev(R, torch_dev)
+        p = sva.default_params(D=D, subpixel=1)
+        outs = []
+        for x in (a, b):
+            disp = torch.zeros((H, W), dtype=torch.int16, device=torch_dev)
+            sub = torch.zeros((H, W), dtype=torch.float32, device=torch_dev)
+            x.disparity_sgm_d(dL.data_ptr(), dR.data_ptr(), W, H, W, p, disp.data_ptr(),
+                              sub.data_ptr())
+            x.synchronize()
+            outs.append((disp.cpu().numpy(), sub.cpu().numpy()))
+        assert np.array_equal(outs[0][0], outs[1][0])
+        assert np.array_equal(outs[0][1], outs[1][1])
+    finally:
+        for x in (a, b, c):
+            x.close()
