@@ -215,8 +215,11 @@ constexpr size_t kBatchMaxBytes = (size_t)24 << 30;
 // Buffer sets timed (the first allocation plus trials - 1 more) when a frame's
 // stage buffers reach kPlacementMinBytes.  At 4K D=256 the path kernel ran
 // 4.28-4.98 ms on twelve allocations of the same buffers, stable within each
-// (profiles/r06_v6/probe_4k_alloc.log.txt); 1080p D=128 (1.6 GB) shows no
-// such spread.
+// (profiles/r06_v6/probe_4k_alloc.log.txt); with the check, 4.23-4.28 ms in
+// three processes against 4.30 / 4.86 / 4.87 without (profiles/r06_v9/4k_t*).
+// 1080p D=128 (1.6 GB) has no such spread: its trials ran 0.502-0.510 ms and
+// the bench line did not move with the check forced on there (0.8816-0.8827
+// vs 0.8772-0.879 ms per frame, profiles/r06_v9/1080_t*), hence the threshold.
 constexpr int kPlacementTrials = 4;
 constexpr size_t kPlacementMinBytes = (size_t)4 << 30;
 
