@@ -261,3 +261,21 @@ def test_engine_counters_skipped_off_the_live_route(bench, monkeypatch):
     bench.attach_engine(a, out, {}, 1)
     bench.attach_engine(args("live"), out, {}, 2)
     assert not called and "valu_roofline" not in out
+
+
+def test_placement_report(bench):
+    """The bench line's `placement` field: the kept and slowest trial times of
+    sva_reserve's placement check, per context; absent when no context ran it."""
+    import stereovisionarray_amd as sva
+
+    class FakeCtx:
+        def __init__(self, kept, worst):
+            self.v = {sva.SVA_DEBUG_PLACEMENT_NS: kept, sva.SVA_DEBUG_PLACEMENT_WORST_NS: worst}
+
+        def get_debug(self, key):
+            return self.v[key]
+
+    assert bench.placement_report([FakeCtx(0, 0)]) is None
+    r = bench.placement_report([FakeCtx(4_193_100, 4_838_900), FakeCtx(0, 0)])
+    assert r["contexts"] == [{"kept_ms": 4.1931, "worst_ms": 4.8389}]
+    assert "fastest set is kept" in r["note"]
