@@ -100,8 +100,9 @@ const char* sva_status_string(int status);
 /* Pre-size the workspace for W x H x D (optional; calls grow it on demand).
  * When the frame's stage buffers (cost volume, diagonal path volumes,
  * checkpoints) reach 4 GiB, reserve also checks their placement: it times the
- * path kernel on the buffers it got and on up to three further allocations of
- * them, keeps the fastest set and frees the others (at 4K
+ * path kernel on the buffers it got and on up to five further allocations of
+ * them (all held until it chooses, while a quarter of the device memory stays
+ * free), keeps the fastest set and frees the others (at 4K
  * D=256 the kernel's rate depends on which physical pages the 10.6 GB of
  * volumes land on, 4.3-4.9 ms, and not on anything else measured).  A few
  * tens of ms, once; SVA_DEBUG_PLACEMENT_TRIALS sets the count (1 = off). */
@@ -151,7 +152,7 @@ int sva_kernel_time(void* ctx, const char* name, double* total_ms, int64_t* coun
  *                            has finished its queued work (hipStreamQuery),
  *                            else 0.
  *   SVA_DEBUG_PLACEMENT_TRIALS  set: buffer sets sva_reserve's placement check
- *                            times (1..8; 1 = no check; 0 = the default, 4).
+ *                            times (1..8; 1 = no check; 0 = the default, 6).
  *   SVA_DEBUG_PLACEMENT_NS   get: the path kernel's time on the set the last
  *                            check kept, ns (0: no check ran).
  *   SVA_DEBUG_PLACEMENT_WORST_NS  get: the slowest set that check timed, ns. */

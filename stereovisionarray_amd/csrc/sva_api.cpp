@@ -637,47 +637,67 @@ int time_stage_set(Ctx* c, int W, int H, int D, int64_t* ns) {
 }
 
 // sva_reserve's placement check (include/sva.h): keep the
-// fastest of `trials` allocations of the stage buffers.  Every set stays
-// allocated while the next is taken, so each trial gets other physical pages.
+// fastest of `trials` allocations of the stage buffers.  Every trial set stays
+// allocated until the choice is made, so each one lands on pages no earlier
+// set holds; a trial is taken only while the device keeps a quarter of its
+// memory (at least 16 GiB) free beside it.
 int place_stage_buffers(Ctx* c, int W, int H, int D, int trials) {
+    struct Set {
+        DevBuf cost, paths, ckpt;
+        int64_t ns = 0;
+    };
     const bool timing = c->timer.enabled;
     c->timer.enabled = false;                 // the trials are not the caller's launches
-    int64_t best = 0, worst = 0;
-    int rc = time_stage_set(c, W, H, D, &best);
-    worst = best;
+    std::vector<Set> sets(1);
+    int rc = time_stage_set(c, W, H, D, &sets[0].ns);
+    const size_t set_bytes = c->cost.bytes + c->paths.bytes + c->ckpt.bytes;
     for (int t = 1; rc == SVA_OK && t < trials; t++) {
-        DevBuf cost, paths, ckpt;
-        cost.flags = c->cost.flags;
-        paths.flags = c->paths.flags;
-        ckpt.flags = c->ckpt.flags;
-        if (cost.ensure(c->cost.bytes) != hipSuccess || paths.ensure(c->paths.bytes) != hipSuccess ||
-            ckpt.ensure(c->ckpt.bytes) != hipSuccess) {
-            cost.release();                   // no room for another set: keep the current one
-            paths.release();
-            ckpt.release();
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) break;
+        const size_t keep = std::max(total_b / 4, (size_t)16 << 30);
+        if (free_b < set_bytes + keep) break;
+        Set n;
+        n.cost.flags = c->cost.flags;
+        n.paths.flags = c->paths.flags;
+        n.ckpt.flags = c->ckpt.flags;
+        if (n.cost.ensure(c->cost.bytes) != hipSuccess || n.paths.ensure(c->paths.bytes) != hipSuccess ||
+            n.ckpt.ensure(c->ckpt.bytes) != hipSuccess) {
+            n.cost.release();                 // no room for another set: stop here
+            n.paths.release();
+            n.ckpt.release();
             (void)hipGetLastError();
             break;
         }
-        std::swap(c->cost, cost);
-        std::swap(c->paths, paths);
-        std::swap(c->ckpt, ckpt);
-        int64_t ns = 0;
-        rc = time_stage_set(c, W, H, D, &ns);
-        if (rc == SVA_OK) worst = std::max(worst, ns);
-        if (rc == SVA_OK && ns < best) {
-            best = ns;                        // keep the trial, free the old set
-        } else {
-            std::swap(c->cost, cost);         // keep the old set, free the trial
-            std::swap(c->paths, paths);
-            std::swap(c->ckpt, ckpt);
-        }
-        cost.release();
-        paths.release();
-        ckpt.release();
+        // time the new set in the context's slots; sets[0] keeps the first set
+        std::swap(c->cost, n.cost);
+        std::swap(c->paths, n.paths);
+        std::swap(c->ckpt, n.ckpt);
+        rc = time_stage_set(c, W, H, D, &n.ns);
+        std::swap(c->cost, n.cost);
+        std::swap(c->paths, n.paths);
+        std::swap(c->ckpt, n.ckpt);
+        sets.push_back(n);
     }
     c->timer.enabled = timing;
+    size_t best = 0;
+    int64_t worst = sets[0].ns;
+    for (size_t i = 1; i < sets.size(); i++) {
+        if (sets[i].ns < sets[best].ns) best = i;
+        worst = std::max(worst, sets[i].ns);
+    }
+    if (rc == SVA_OK && best != 0) {          // the context takes the fastest set
+        std::swap(c->cost, sets[best].cost);
+        std::swap(c->paths, sets[best].paths);
+        std::swap(c->ckpt, sets[best].ckpt);
+    }
+    const int64_t kept = sets[rc == SVA_OK ? best : 0].ns;
+    for (size_t i = 1; i < sets.size(); i++) {  // every other set (the old slots included)
+        sets[i].cost.release();
+        sets[i].paths.release();
+        sets[i].ckpt.release();
+    }
     if (rc != SVA_OK) return rc;
-    c->placement_ns = best;
+    c->placement_ns = kept;
     c->placement_worst_ns = worst;
     return SVA_OK;
 }

@@ -220,7 +220,10 @@ constexpr size_t kBatchMaxBytes = (size_t)24 << 30;
 // 1080p D=128 (1.6 GB) has no such spread: its trials ran 0.502-0.510 ms and
 // the bench line did not move with the check forced on there (0.8816-0.8827
 // vs 0.8772-0.879 ms per frame, profiles/r06_v9/1080_t*), hence the threshold.
-constexpr int kPlacementTrials = 4;
+// 6 sets, all held until the choice (so no trial reuses another's pages):
+// with 4 sets, one set freed before the next was taken, a later box kept a
+// 4.51 ms set (slowest 4.84; profiles/r06_final3/4k_d256.log.txt).
+constexpr int kPlacementTrials = 6;
 constexpr size_t kPlacementMinBytes = (size_t)4 << 30;
 
 // ---- census.hip / census_cost.hip / cost.hip ------------
