@@ -222,7 +222,7 @@ constexpr size_t kBatchMaxBytes = (size_t)24 << 30;
 // vs 0.8772-0.879 ms per frame, profiles/r06_v9/1080_t*), hence the threshold.
 // 6 sets, all held until the choice (so no trial reuses another's pages):
 // with 4 sets, one set freed before the next was taken, a later box kept a
-// 4.51 ms set (slowest 4.84; profiles/r06_final3/4k_d256.log.txt).
+// 4.51 ms set (slowest 4.84; profiles/r06_final3/4k_d256_four_sets_freed.log.txt).
 constexpr int kPlacementTrials = 6;
 constexpr size_t kPlacementMinBytes = (size_t)4 << 30;
 
