@@ -699,6 +699,7 @@ int place_stage_buffers(Ctx* c, int W, int H, int D, int trials) {
     if (rc != SVA_OK) return rc;
     c->placement_ns = kept;
     c->placement_worst_ns = worst;
+    c->placement_paths = c->paths.ptr;
     return SVA_OK;
 }
 
@@ -718,9 +719,11 @@ int sva_reserve(void* ctx, int W, int H, int D) {
     const size_t ckb = tg.hck_bytes + tg.vck_bytes + tg.dck_bytes;
     SVA_HIP(c, c->paths.ensure(nv * tg.nvol), "reserve");
     SVA_HIP(c, c->ckpt.ensure(ckb), "reserve");
+    // (once per allocation: a repeated reserve of a size the buffers already
+    // hold keeps the set the last check chose)
     const int trials = c->placement_trials > 0 ? c->placement_trials : tune::kPlacementTrials;
     if (trials > 1 && wta_hv_supported(D) && nv < ((size_t)1 << 32) &&
-        nv + nv * tg.nvol + ckb >= tune::kPlacementMinBytes)
+        nv + nv * tg.nvol + ckb >= tune::kPlacementMinBytes && c->paths.ptr != c->placement_paths)
         return place_stage_buffers(c, W, H, D, trials);
     return SVA_OK;
 }

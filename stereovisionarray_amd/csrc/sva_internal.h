@@ -90,6 +90,7 @@ struct Ctx {
     // and the kept / slowest set's path-kernel time of the last check (ns)
     int placement_trials = 0;
     int64_t placement_ns = 0, placement_worst_ns = 0;
+    const void* placement_paths = nullptr;   // the path buffer the last check chose
 };
 
 // Which launches a timing mode records: SVA_TIMING_ALL every one,

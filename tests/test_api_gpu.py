@@ -191,6 +191,8 @@ def test_reserve_placement_check(sva, torch_dev):
         worst = a.get_debug(sva.SVA_DEBUG_PLACEMENT_WORST_NS)
         assert 0 < kept <= worst
         assert 1e5 < kept < 1e8                      # 0.1-100 ms: a real 4K D=256 launch
+        a.reserve(W, H, D)                           # same buffers: no second check
+        assert a.get_debug(sva.SVA_DEBUG_PLACEMENT_NS) == kept
         b.set_debug(sva.SVA_DEBUG_PLACEMENT_TRIALS, 1)
         b.reserve(W, H, D)
         assert b.get_debug(sva.SVA_DEBUG_PLACEMENT_NS) == 0
