@@ -108,6 +108,11 @@ constexpr int kStripCols = 128;
 // minimum waves per SIMD asked of the compiler (launch bounds)
 constexpr int kStripMinWaves = 3;
 // log2 of the tile rows and of the checkpoint segment (tiles are 16 x 2^this).
+// Round 6 re-check of 16 x 16 (checkpoints every 16: -0.13 GB per 1080p
+// D=128 frame, now that wta_hv streams its bytes; profiles/r06_v11/), frame
+// ms 16x8 / 16x16: 1080p D=128 0.8806 / 0.899 (sgm_paths 0.516 -> 0.500,
+// wta_hv 0.252 -> 0.283 at 2 workgroups per CU by its 64 KB of LDS), D=64
+// 0.511 / 0.512, 640x480 D=64 0.127 / 0.138.  Stays 3.
 constexpr int kWtahvTileLog2 = 3;
 constexpr int kWtahvTileLog2Wide = 3;      // D > 128
 // Prefetch depth (pixels) of the four diagonal-volume loads in the last pass.
