@@ -287,9 +287,19 @@ __device__ __forceinline__ void sgm_step_c(const unsigned (&c)[DPL / 2], unsigne
     // K = -(m * 0x10001) in one v_mul_i32_i24 (m < 2^10; the literal's low 24
     // bits are -65537), and m + P2 in both halves = P2 * 0x10001 - K: two VALU
     // where m | m << 16, its negation and the sum took three plus a copy of P2
-    unsigned K;
+    unsigned K, mP2;
     asm("v_mul_i32_i24_e32 %0, 0xfffeffff, %1" : "=v"(K) : "v"(m));
-    const unsigned mP2 = P2 * 0x10001u - K;
+    if constexpr (tune::kStepMadP2 != 0) {
+        // m + P2 in both halves straight from m (v_mad_u32_u24: m * 0x10001 +
+        // P2 * 0x10001, beside K instead of after it): one dependent
+        // instruction less on the step's critical path m -> min3 -> add3
+        // (asm: in plain C the compiler splits m * 0x10001 into a shift-add;
+        // here it re-materialises the uniform P2 * 0x10001 with one v_mov
+        // per step, off the critical path)
+        asm("v_mad_u32_u24 %0, %1, %2, %3" : "=&v"(mP2) : "v"(m), "s"(0x10001u), "v"(P2 * 0x10001u));
+    } else {
+        mP2 = P2 * 0x10001u - K;
+    }
     // Stage-major over the NP independent pairs, and a min TREE below: each
     // packed op's result is consumed one pair later, not by the next
     // instruction (gfx950 puts an s_nop between dependent VOP3P ops).

@@ -29,6 +29,15 @@ constexpr int kStepAddU32 = 1;
 // (sgm_paths -2.5 %), D=192 1.3132 / 1.3205, D=256 1.7015 / 1.7098 and
 // 1.6991 / 1.7094, 640x480 D=64 0.1260 / 0.1276 and 0.1274 / 0.1297.
 constexpr int kSplitPairs = 1;
+// m + P2 of the step as one v_mad_u32_u24 from m (1), beside K, instead of
+// P2 * 0x10001 - K after it (0): the chain row minimum -> m + P2 -> min3 ->
+// add3 one instruction shorter, for the latency-bound lines of small frames,
+// at one v_mov per step (the uniform P2 * 0x10001 re-materialised in a VGPR).
+// Frame ms on / off (profiles/r06_v12/): 640x480 D=64 0.1272 / 0.1263,
+// 960x540 D=64 0.1653 / 0.1654, 1080p D=64 0.5151 / 0.5078 (sgm_paths
+// 0.289 / 0.281), 1080p D=128 0.8823 / 0.8818: a lone line's step is not
+// bound by that chain.  Off.
+constexpr int kStepMadP2 = 0;
 // Prefetch ring depth in steps, per line kind and disparities per lane
 // (D = 16 * DPL).  Horizontal lines are few (2H) and long (W steps) and run
 // alone once the vertical/diagonal lines drain, so they get the deeper ring.
