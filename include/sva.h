@@ -104,8 +104,11 @@ const char* sva_status_string(int status);
  * them (all held until it chooses, while a quarter of the device memory stays
  * free), keeps the fastest set and frees the others (at 4K
  * D=256 the kernel's rate depends on which physical pages the 10.6 GB of
- * volumes land on, 4.3-4.9 ms, and not on anything else measured).  A few
- * tens of ms, once; SVA_DEBUG_PLACEMENT_TRIALS sets the count (1 = off). */
+ * volumes land on, 4.3-4.9 ms, and not on anything else measured).  About
+ * 0.2 s at 4K D=256, once per allocation; the call then returns after the
+ * trial launches have finished on the context stream (work queued on that
+ * stream before it runs first).  SVA_DEBUG_PLACEMENT_TRIALS sets the count
+ * (1 = off). */
 int sva_reserve(void* ctx, int width, int height, int D);
 
 /* Path-aggregation route of sva_disparity_sgm*.  COST_VOLUME (= AUTO, the
