@@ -245,6 +245,165 @@ __global__ __launch_bounds__(CC_BLOCK) void census_cost_mma_kernel(
     }
 }
 
+// The same census + cost with the two phases on different waves (round 6,
+// tune::kCensusCostWS): a 512-thread workgroup whose waves 0-3 form the census
+// operand rows of row p + 1 while waves 4-7 multiply row p's (two operand
+// buffers) and store their own residue class's pixels, one barrier per row
+// instead of two.  PXB = 64: each MFMA wave's 16 pixels are its own class, so
+// it stores them behind a wave barrier.  Bit-identical to the kernel above.
+template <int NC, int DIR>
+__global__ __launch_bounds__(2 * CC_BLOCK) void census_cost_ws_kernel(
+    const uint8_t* __restrict__ left, const uint8_t* __restrict__ right, int W, int H,
+    size_t pitch, int dmin, int rows, int dreal, uint8_t* __restrict__ C) {
+    constexpr int D = NC * 16;
+    constexpr int PXB = 64;
+    constexpr int T = (D + 60 + 15) / 16;
+    constexpr int NWM = PXB + D - 1;
+    constexpr int NWMP = (16 + NWM + 4 + 15) / 16 * 16;
+    constexpr int RW = (NWM + 8 + 4 + 3) / 4 * 4;
+    constexpr int LW = (PXB + 8 + 4 + 3) / 4 * 4;
+    constexpr int SPAN = NWM + 8 + PXB + 8;
+    constexpr int LOADS = (SPAN + CC_BLOCK - 1) / CC_BLOCK;
+    constexpr int NWORDS = PXB + NWM;
+    constexpr int WPT = (NWORDS + CC_BLOCK - 1) / CC_BLOCK;
+    constexpr int S4 = NC * 4 + 7;
+    __shared__ __attribute__((aligned(16))) uint8_t ringR[RING][RW];
+    __shared__ __attribute__((aligned(16))) uint8_t ringL[RING][LW];
+    __shared__ __attribute__((aligned(16))) uint8_t opA[2][4 * NWMP * 16];
+    __shared__ __attribute__((aligned(16))) uint8_t opB[2][4 * PXB * 16];
+    __shared__ unsigned stg[PXB * S4];
+
+    const int bpr = (W + PXB - 1) / PXB;
+    const int bx = blockIdx.x % bpr, by = blockIdx.x / bpr;
+    const int x0 = bx * PXB, y0 = by * rows;
+    const int nrows = min(H, y0 + rows) - y0;
+    const int t = threadIdx.x, grp = t >> 8, tl = t & (CC_BLOCK - 1);   // grp: wave-uniform
+    const int xlo = DIR > 0 ? x0 + dmin : x0 + 1 - dmin - D;
+    const int cbR = xlo - HX, cbL = x0 - HX;
+
+    auto fetch = [&](int gy, uint8_t (&v)[LOADS]) {
+#pragma unroll
+        for (int k = 0; k < LOADS; k++) {
+            const int i = tl + k * CC_BLOCK;
+            int col;
+            const uint8_t* img;
+            if (i < NWM + 8) { col = cbR + i; img = right; }
+            else { col = cbL + (i - (NWM + 8)); img = left; }
+            v[k] = (i < SPAN && (unsigned)col < (unsigned)W && (unsigned)gy < (unsigned)H)
+                       ? img[(size_t)gy * pitch + col] : 0;
+        }
+    };
+    auto stage = [&](int gy, const uint8_t (&v)[LOADS]) {
+        const int slot = gy & (RING - 1);
+#pragma unroll
+        for (int k = 0; k < LOADS; k++) {
+            const int i = tl + k * CC_BLOCK;
+            if (i < NWM + 8) ringR[slot][i] = v[k];
+            else if (i < SPAN) ringL[slot][i - (NWM + 8)] = v[k];
+        }
+    };
+    // census operand rows of image row y into buffer b (group 0)
+    auto census_row = [&](int y, int b) {
+        const bool yin = y >= HY && y < H - HY;
+        const unsigned* rR[7];
+        const unsigned* rL[7];
+#pragma unroll
+        for (int dy = -HY; dy <= HY; dy++) {
+            rR[dy + HY] = reinterpret_cast<const unsigned*>(ringR[(y + dy) & (RING - 1)]);
+            rL[dy + HY] = reinterpret_cast<const unsigned*>(ringL[(y + dy) & (RING - 1)]);
+        }
+#pragma unroll
+        for (int k = 0; k < WPT; k++) {
+            const int w = tl + k * CC_BLOCK;
+            unsigned d[16];
+            if (w < PXB) {
+                const int lp = 4 * (w % (PXB / 4)) + w / (PXB / 4), x = x0 + lp;
+                if (yin && x >= HX && x < W - HX) census_bytes<true>(rL, lp, d);
+                else census_zero<true>(d);
+                put_operand_row(opB[b], PXB, w, d);
+            } else if (w < NWORDS) {
+                const int i = w - PXB, col = xlo + i;
+                if ((unsigned)col >= (unsigned)W) census_outside(d);
+                else if (yin && col >= HX && col < W - HX) census_bytes<false>(rR, i, d);
+                else census_zero<false>(d);
+                put_operand_row(opA[b], NWMP, 16 + i, d);
+            }
+        }
+    };
+
+    // prologue: image rows y0 - 3 .. y0 + 4 (the whole ring: the census of
+    // rows 0 and 1), then row 0's operands
+    {
+        uint8_t v[4][LOADS];
+#pragma unroll
+        for (int r = 0; r < 4; r++) fetch(y0 - HY + 4 * grp + r, v[r]);
+#pragma unroll
+        for (int r = 0; r < 4; r++) stage(y0 - HY + 4 * grp + r, v[r]);
+    }
+    __syncthreads();
+    if (grp == 0) census_row(y0, 0);
+    uint8_t pre[LOADS];
+    if (grp == 1) fetch(y0 + HY + 2, pre);
+    __syncthreads();
+
+    const int wv = (t >> 6) & 3, l = t & 63, ln = l & 15, lq = l >> 4;
+    for (int p = 0; p < nrows; p++) {
+        if (grp == 0) {
+            if (p + 1 < nrows) census_row(y0 + p + 1, (p + 1) & 1);
+        } else {
+            const int b = p & 1, c = wv;                 // this wave's residue class
+            const v4i zero = {0, 0, 0, 0};
+            const int m = DIR > 0 ? ln : 15 - ln;
+            const v4i bf = *reinterpret_cast<const v4i*>(&opB[b][(lq * PXB + c * (PXB / 4) + m) * 16]);
+            unsigned* dst = &stg[(c * (PXB / 4) + ln) * S4];
+            constexpr int G = 4;
+#pragma unroll
+            for (int g = 0; g < T; g += G) {
+                v4i acc[G];
+#pragma unroll
+                for (int i = 0; i < G && g + i < T; i++) {
+                    const int R = 16 * (g + i) + ln;
+                    const int idx = DIR > 0 ? c + R : c + D + 59 - R;
+                    const v4i af = *reinterpret_cast<const v4i*>(&opA[b][(lq * NWMP + 16 + idx) * 16]);
+                    acc[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf, zero, 0, 0, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < G && g + i < T; i++) {
+                    const int j = 4 * (g + i) + lq - ln;
+                    unsigned wd = (unsigned)acc[i][0] | ((unsigned)acc[i][1] << 8);
+                    wd |= ((unsigned)acc[i][2] << 16) | ((unsigned)acc[i][3] << 24);
+                    dst[(unsigned)j < (unsigned)(NC * 4) ? j : NC * 4 + lq] = wd;   // else: dump
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // this wave's 16 pixels (class c) leave as whole lines: the lanes
+            // read other lanes' staging words (same wave: LDS order, no barrier
+            // instruction)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int y = y0 + p;
+#pragma unroll
+            for (int k = 0; k < 16 * NC / 64; k++) {
+                const int ch = l + 64 * k;
+                const int sl = ch / NC, ci = ch % NC;      // slot sl of the class: pixel lane n = sl
+                const int lp = 4 * (DIR > 0 ? sl : 15 - sl) + c, x = x0 + lp;
+                if (x >= W) continue;
+                const unsigned* src = &stg[(c * (PXB / 4) + sl) * S4 + 4 * ci];
+                unsigned out[4] = {src[0], src[1], src[2], src[3]};
+                if (dreal < D) {                 // padded disparities: cost 255
+#pragma unroll
+                    for (int q = 0; q < 4; q++) out[q] |= pad_bytes(16 * ci + 4 * q, dreal);
+                }
+                store16_nt(C + ((size_t)y * W + x) * D + 16 * ci, out);
+            }
+            stage(y0 + p + HY + 2, pre);
+            if (p + 1 < nrows) fetch(y0 + p + HY + 3, pre);
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 bool census_cost_supported(int D) { return D == 64 || D == 128 || D == 192 || D == 256; }
@@ -253,7 +412,9 @@ hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right,
                               size_t pitch, int D, int dmin, int dir, uint8_t* C, int dreal) {
     if (dreal <= 0) dreal = D;
     ScopedKernelTimer t(c, "cost");
-    const int px = D == 64 ? mma_px<4>() : D == 128 ? mma_px<8>() : D == 192 ? mma_px<12>() : mma_px<16>();
+    // the wave-specialised kernel for D < 256 (PXB 64), tune::kCensusCostWS
+    const bool ws = tune::kCensusCostWS != 0 && D <= 192;
+    const int px = ws ? 64 : D == 64 ? mma_px<4>() : D == 128 ? mma_px<8>() : D == 192 ? mma_px<12>() : mma_px<16>();
     const long long bpr = (W + px - 1) / px;
     const int rows = bpr * ((H + tune::kCensusCostRows - 1) / tune::kCensusCostRows) >=
                              tune::kCensusCostMinGroups
@@ -261,7 +422,16 @@ hipError_t launch_census_cost(Ctx& c, const uint8_t* left, const uint8_t* right,
                          : tune::kCensusCostRowsSmall;
     const dim3 grid((unsigned)(bpr * ((H + rows - 1) / rows)));
 #define SVA_CC_MMA(NC_)                                                                            \
-    if (dir > 0)                                                                                   \
+    if (ws && NC_ <= 12) {                                                                         \
+        if (dir > 0)                                                                               \
+            hipLaunchKernelGGL((census_cost_ws_kernel<(NC_ <= 12 ? NC_ : 12), 1>), grid,            \
+                               dim3(2 * CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin,    \
+                               rows, dreal, C);                                                    \
+        else                                                                                       \
+            hipLaunchKernelGGL((census_cost_ws_kernel<(NC_ <= 12 ? NC_ : 12), -1>), grid,           \
+                               dim3(2 * CC_BLOCK), 0, c.stream, left, right, W, H, pitch, dmin,    \
+                               rows, dreal, C);                                                    \
+    } else if (dir > 0)                                                                            \
         hipLaunchKernelGGL((census_cost_mma_kernel<NC_, 1>), grid, dim3(CC_BLOCK), 0, c.stream, left, \
                            right, W, H, pitch, dmin, rows, dreal, C);                             \
     else                                                                                           \

@@ -296,6 +296,14 @@ constexpr int kCostStoreNT = 1;
 // 0.0918, D=192 0.127 -> 0.1247, D=256 0.1418 -> 0.1376, 4K D=256 0.5376 ->
 // 0.5213, D=64 unchanged.
 constexpr int kCensusCostSlotOrder = 1;
+// census_cost with the census and the multiply on different waves
+// (census_cost_ws_kernel: 512 threads, two operand buffers, one barrier per
+// row), D <= 192.  Bit-exact (290 census / SGM / any-D / config tests with it
+// on) and slower, census_cost ms on / off (profiles/r06_v14/): 1080p D=128
+// 0.0947 / 0.0874, D=64 0.0733 / 0.0639, D=192 0.1489 / 0.1233, 640x480 D=64
+// 0.0186 / 0.0166, 4K D=128 0.381 / 0.346 -- half the waves idle in each
+// phase cost more than the second barrier and the serialised phases.  Off.
+constexpr int kCensusCostWS = 0;
 // census_cost2.hip (2-D array steps): adjacent lattice lines per workgroup,
 // which share one staged image patch.
 constexpr int kCensusCost2Lines = 8;
